@@ -1,0 +1,212 @@
+/*
+ * unet_hip.h — C-ABI of libunet_hip.so, the MI355X (gfx950) engine for the
+ * separable-conv U-Net hot path of planck-epoch/unet-image-segmentation.
+ *
+ * The reference has no native code and no FFI: every op on the path is an
+ * implicit TensorFlow kernel emitted by a Keras layer.  Each entry point below
+ * names the Keras layer / reference function it replaces (file:line in the
+ * reference).  The reference-side binding a maintainer would add (ctypes) is
+ * shown in INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *   - tensors are NHWC float32, dense (row stride = channel count), device
+ *     memory owned by the caller; nothing here allocates device memory;
+ *   - weights use the Keras layouts (see each function);
+ *   - every call is asynchronous on `stream` (a hipStream_t; NULL = default);
+ *   - return 0 on success, < 0 for an invalid argument, > 0 for a hipError_t;
+ *     unet_last_error() gives a thread-local message for the last failure;
+ *   - reductions are deterministic (fixed order, no float atomics): the same
+ *     inputs give bitwise-identical outputs run to run;
+ *   - ops needing scratch take (ws, ws_bytes); query the size with the
+ *     matching *_workspace() function.
+ */
+#ifndef UNET_HIP_H
+#define UNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UNET_ABI_VERSION 1
+
+typedef void* unet_stream_t; /* hipStream_t */
+
+/* ---------------------------------------------------------------------------
+ * Activation views.  Producers store raw (pre-BatchNorm) conv outputs; a
+ * consumer reads the activation it needs through a view, which applies the
+ * BatchNormalization affine + ReLU of model/u_net.py:22-25 on load, and
+ * optionally MaxPooling2D (u_net.py:69), Concatenate (u_net.py:95-96) and
+ * Dropout (u_net.py:77-78, 97-98).  The logical tensor is (n, h, w, c0 + c1).
+ * ------------------------------------------------------------------------ */
+enum {
+    UNET_VIEW_PLAIN = 0,       /* x = src0                                    */
+    UNET_VIEW_BNRELU = 1,      /* x = relu(src0 * scale0 + shift0)            */
+    UNET_VIEW_POOL_BNRELU = 2, /* x = maxpool2x2(relu(src0*scale0+shift0)),
+                                  src0 is (n, 2h, 2w, c0)                     */
+    UNET_VIEW_CONCAT = 3       /* x = [src0 (raw, c0) | relu(src1*scale1+shift1) (c1)] */
+};
+
+typedef struct unet_view {
+    int32_t mode;
+    int32_t c0;
+    int32_t c1;          /* CONCAT only, else 0 */
+    int32_t reserved0;
+    const float* src0;
+    const float* scale0; /* per-channel, BNRELU / POOL_BNRELU */
+    const float* shift0;
+    const float* src1;   /* CONCAT: skip tensor (n, h, w, c1) */
+    const float* scale1;
+    const float* shift1;
+    float drop_rate;     /* Dropout on the logical tensor; 0 = off */
+    int32_t reserved1;
+    uint64_t drop_seed;  /* keep(i) = u(splitmix64(seed + i*golden)) >= rate */
+} unet_view;
+
+int unet_abi_version(void);
+const char* unet_last_error(void);
+
+/* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
+ * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers
+ * read views directly); it serves eager conv_block outputs and inspection.                 */
+int unet_view_materialize(const unet_view* x, int n, int h, int w, float* out,
+                          unet_stream_t stream);
+
+/* ----- SeparableConv2D(f, 3, padding='same') — model/u_net.py:14-20 --------
+ * Depthwise half: y[n,h,w,c] = sum_{i,j<3} x[n,h+i-1,w+j-1,c] * k[i,j,c],
+ * zero padding.  dw_kernel is Keras `depthwise_kernel` (3, 3, C, 1).       */
+int unet_dwconv3x3_fwd(const unet_view* x, int n, int h, int w,
+                       const float* dw_kernel, float* y, unet_stream_t stream);
+
+/* Gradient w.r.t. the view's input.  Routing by view mode:
+ *   PLAIN / BNRELU : dx0 (n,h,w,c0) = d(logical x)   (store)
+ *   POOL_BNRELU    : dx0 (n,2h,2w,c0) += grad routed to the first max of each
+ *                    2x2 window (accumulates: the skip path stored first)
+ *   CONCAT         : dx0 (n,h,w,c0) = grad of the upsample half (store),
+ *                    dx1 (n,h,w,c1) = grad of the skip half (store)
+ * Dropout (if the view has it) is applied to the gradient first.          */
+int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w,
+                            const float* dw_kernel, const float* dy,
+                            float* dx0, float* dx1, unet_stream_t stream);
+
+size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c);
+/* d_dw_kernel (3,3,C,1) = sum over pixels of x(shifted) * dy (overwrites). */
+int unet_dwconv3x3_bwd_filter(const unet_view* x, int n, int h, int w,
+                              const float* dy, float* d_dw_kernel,
+                              void* ws, size_t ws_bytes, unet_stream_t stream);
+
+/* Pointwise half: z[m, co] = sum_ci y[m, ci] * k[ci, co];  pw_kernel is Keras
+ * `pointwise_kernel` (1, 1, Cin, Cout).  If bn_partials != NULL the epilogue
+ * also writes per-tile BatchNorm statistics (count-weighted mean and M2 per
+ * channel) for unet_bn_finalize.                                            */
+size_t unet_bn_partials_size(int64_t m, int c); /* bytes of bn_partials */
+int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout,
+                       const float* pw_kernel, float* z, float* bn_partials,
+                       unet_stream_t stream);
+/* dy[m, ci] = sum_co dz[m, co] * k[ci, co] */
+int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout,
+                            const float* pw_kernel, float* dy,
+                            unet_stream_t stream);
+size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout);
+/* d_pw_kernel[ci, co] = sum_m y[m, ci] * dz[m, co] (overwrites) */
+int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
+                              int cin, int cout, float* d_pw_kernel,
+                              void* ws, size_t ws_bytes, unet_stream_t stream);
+
+/* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
+ * momentum 0.99, epsilon 1e-3, biased batch variance for both the output
+ * and the moving-variance update).  Training: reduces bn_partials into the
+ * batch mean / variance, writes mean, rstd = 1/sqrt(var+eps), and the affine
+ * scale = gamma*rstd, shift = beta - mean*scale consumed by views; updates
+ * moving stats when update_moving != 0.  gamma == NULL means
+ * use_batch_norm=False: scale = 1, shift = beta (the sepconv bias).        */
+int unet_bn_finalize(const float* bn_partials, int64_t m, int c,
+                     const float* gamma, const float* beta, float eps,
+                     float momentum, float* moving_mean, float* moving_var,
+                     int update_moving, float* mean, float* rstd,
+                     float* scale, float* shift, unet_stream_t stream);
+/* Inference: scale/shift from the moving statistics. */
+int unet_bn_infer_params(const float* gamma, const float* beta,
+                         const float* moving_mean, const float* moving_var,
+                         int c, float eps, float* scale, float* shift,
+                         unet_stream_t stream);
+/* Backward of a = dropout(relu(z*scale+shift)):
+ *   g = da * keep/(1-rate) * [z*scale+shift > 0]
+ *   dbeta = sum g, dgamma = sum g*xhat (xhat = (z-mean)*rstd)
+ *   dz = scale*(g - dbeta/M - xhat*dgamma/M)    (use_bn != 0)
+ *   dz = g, dbeta = sum g, dgamma untouched       (use_bn == 0, bias grad)  */
+size_t unet_bn_relu_bwd_workspace(int64_t m, int c);
+int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int c,
+                     const float* mean, const float* rstd, const float* scale,
+                     const float* shift, int use_bn, float drop_rate,
+                     uint64_t drop_seed, float* dgamma, float* dbeta,
+                     float* dz, void* ws, size_t ws_bytes,
+                     unet_stream_t stream);
+
+/* ----- Conv2DTranspose(f, 2, strides=2, padding='same') — u_net.py:88-94 --
+ * out[n, 2i+a, 2j+b, co] = bias[co] + sum_ci x[n,i,j,ci] * k[a,b,co,ci];
+ * kernel is Keras (2, 2, Cout, Cin), x a view of (n, h, w, Cin).           */
+int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w,
+                               int cout, const float* kernel,
+                               const float* bias, float* out,
+                               unet_stream_t stream);
+size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int cin,
+                                            int cout);
+/* dx (n,h,w,Cin) = grad w.r.t. the view output (NULL: skip); dkernel, dbias
+ * overwrite. */
+int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w,
+                               int cout, const float* kernel,
+                               const float* dout, float* dx, float* dkernel,
+                               float* dbias, void* ws, size_t ws_bytes,
+                               unet_stream_t stream);
+
+/* ----- Output layer Conv2D(ncls, 1, activation) — u_net.py:105-112 --------
+ * prob = sigmoid(x.k + b) (ncls == 1) or softmax over channels.            */
+int unet_head_fwd(const unet_view* x, int n, int h, int w, int ncls,
+                  const float* kernel, const float* bias, float* prob,
+                  unet_stream_t stream);
+
+/* ----- dice_coef / iou_coef / dice_loss — utils/metrics.py:6-62,
+ * utils/loss.py:9-48.  Per (batch, channel) sums over H, W:
+ * sums[b][c] = {sum t*p, sum t, sum p};  result = {1 - mean dice,
+ * mean dice, mean iou}.  smooth = K.epsilon() = 1e-7 in the reference.     */
+enum { UNET_LOSS_DICE = 0, UNET_LOSS_IOU = 1 };
+size_t unet_dice_workspace(int n, int64_t hw, int ncls);
+int unet_dice_fwd(const float* y_true, const float* y_pred, int n,
+                  int64_t hw, int ncls, float smooth, float* sums,
+                  float* result, void* ws, size_t ws_bytes,
+                  unet_stream_t stream);
+/* Backward of (1 - mean dice) [or 1 - mean iou] through the head
+ * activation and the 1x1 conv: dx (n,h,w,Cin) grad w.r.t. the head input
+ * view; dkernel (1,1,Cin,ncls), dbias (ncls) overwrite.                    */
+size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls);
+int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
+                  const float* kernel, const float* prob,
+                  const float* y_true, const float* sums, float smooth,
+                  int loss_kind, float* dx, float* dkernel, float* dbias,
+                  void* ws, size_t ws_bytes, unet_stream_t stream);
+
+/* ----- keras.metrics.MeanIoU(num_classes) — scripts/train.py:231,
+ * scripts/benchmark.py:237,269.  Confusion counts (rows = true, cols =
+ * pred) accumulate into `confusion` (num_classes^2 uint64).  threshold < 0:
+ * Keras cast semantics (float -> int64 truncation, as in training on raw
+ * probabilities); threshold >= 0: pred = (p > threshold) (benchmark.py:260).
+ * Labels outside [0, num_classes) are skipped.                             */
+int unet_meaniou_update(const float* y_true, const float* y_pred,
+                        int64_t count, int num_classes, float threshold,
+                        uint64_t* confusion, unet_stream_t stream);
+
+/* ----- keras.optimizers.AdamW — scripts/train.py:226 (Keras 3 update):
+ *   p -= p*wd*lr;  g *= grad_scale;  m += (g-m)(1-b1);  v += (g^2-v)(1-b2);
+ *   p -= m*alpha / (sqrt(v) + eps),  alpha = lr*sqrt(1-b2^t)/(1-b1^t).      */
+int unet_adamw_step(float* param, const float* grad, float* m, float* v,
+                    int64_t count, float lr, float weight_decay, float beta1,
+                    float beta2, float eps, float alpha, float grad_scale,
+                    unet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_HIP_H */

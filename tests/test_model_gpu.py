@@ -1,0 +1,166 @@
+"""Whole-model parity of the MI355X engine against the NumPy oracle (float64), through the
+reference's builder API (model/u_net.py U_NET) and the train step of scripts/train.py.
+
+Tolerances (north star: masks within 1e-3 on identical weights/inputs):
+  * inference probabilities: max |p - p_ref| < 1e-3 (measured ~1e-6);
+  * one train step: loss within 1e-5; every gradient tensor within 1e-3 relative L2 norm;
+    post-AdamW weights within 1e-4 relative.
+"""
+import numpy as np
+import pytest
+
+from helpers import f32, host, norm_err, rel_err
+from oracle.unet_ref import UNetOracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _weights_with_stats(model, rng):
+    """Random Keras-initialised weights plus non-trivial BN moving stats / gamma / beta."""
+    w = model.engine.get_weights_dict()
+    for k in w:
+        if k.endswith("moving_mean"):
+            w[k] = (rng.standard_normal(w[k].shape) * 0.2).astype(np.float32)
+        elif k.endswith("moving_variance"):
+            w[k] = (0.5 + rng.random(w[k].shape)).astype(np.float32)
+        elif k.endswith("gamma"):
+            w[k] = (1 + 0.2 * rng.standard_normal(w[k].shape)).astype(np.float32)
+        elif k.endswith("beta") or k.endswith("/bias"):
+            w[k] = (0.1 * rng.standard_normal(w[k].shape)).astype(np.float32)
+    model.engine.set_weights_dict(w)
+    return {k: v.astype(np.float64) for k, v in w.items()}
+
+
+def _data(rng, n, h, w, ncls):
+    x = rng.random((n, h, w, 3), dtype=np.float32)
+    if ncls == 1:
+        y = np.zeros((n, h, w, 1), np.float32)
+        for i in range(n):  # ID-card-like axis-aligned quads (~30% foreground)
+            y0, x0 = rng.integers(0, h // 3), rng.integers(0, w // 3)
+            y[i, y0:y0 + h // 2, x0:x0 + w // 2] = 1.0
+    else:
+        y = np.eye(ncls, dtype=np.float32)[rng.integers(0, ncls, (n, h, w))]
+    return x, y
+
+
+def test_builder_api_and_inference_parity_cfg1():
+    """configs[0]: U_NET((128,128,3), 1) forward on 2 images."""
+    from model.u_net import U_NET, unet
+    with pytest.raises(ValueError):
+        U_NET((128, 128))
+    model = unet(input_size=(128, 128, 3), num_classes=1)
+    assert model.count_params() == 6000028
+    rng = np.random.default_rng(2301)
+    p = _weights_with_stats(model, rng)
+    x, _ = _data(rng, 2, 128, 128, 1)
+    prob = model.predict(x)
+    ref, _, _ = UNetOracle(1).forward(p, x.astype(np.float64), training=False)
+    assert prob.shape == (2, 128, 128, 1)
+    assert np.abs(prob - ref).max() < 1e-3
+    assert np.abs(prob - ref).max() < 2e-5  # in practice fp32 rounding only
+    # binary masks at the reference's threshold (scripts/inference.py:160) agree pixelwise
+    # except where |p - 0.5| is below the numeric noise
+    far = np.abs(ref - 0.5) > 1e-4
+    assert np.array_equal((prob > 0.5)[far], (ref > 0.5)[far])
+
+
+@pytest.mark.parametrize("ncls,use_bn,drop,loss", [(1, True, 0.0, "dice_loss"), (1, True, 0.2, "dice_loss"),
+                                                   (21, True, 0.0, "dice_loss"), (1, False, 0.0, "dice_loss"),
+                                                   (1, True, 0.0, "iou_loss")])
+def test_train_step_parity(ncls, use_bn, drop, loss):
+    from unet_amd.model import UNetModel
+    from unet_amd.optim import AdamW
+    n, hw = 2, 32
+    model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
+    rng = np.random.default_rng(ncls * 13 + int(drop * 10) + use_bn)
+    p = _weights_with_stats(model, rng)
+    x, y = _data(rng, n, hw, hw, ncls)
+    lr, wd = 2e-3, 1e-4
+    model.compile(AdamW(learning_rate=lr, weight_decay=wd), loss)
+    seeds = model.engine.drop_seeds(1)
+    res = model.train_step(x, y).cpu().numpy()
+    torch.cuda.synchronize()
+    grads = {k: host(t) for k, t in model.engine.gvars.items()}
+    neww = model.engine.get_weights_dict()
+
+    orc = UNetOracle(ncls, drop, use_bn)
+    opt = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in p.items() if k in grads}
+    lval, dice, g, newp, _, prob = orc.train_step(p, opt, x.astype(np.float64), y.astype(np.float64), 1, lr, wd,
+                                                  drop_seeds=seeds if drop > 0 else None,
+                                                  loss="dice" if loss == "dice_loss" else "iou")
+    assert abs(res[0] - lval) < 1e-5, (res[0], lval)
+    assert abs(res[1] - dice) < 1e-5
+    bad = {k: norm_err(grads[k], g[k]) for k in g if norm_err(grads[k], g[k]) > 1e-3}
+    assert not bad, bad
+    assert set(g) == set(grads)
+    for k, v in newp.items():
+        assert rel_err(neww[k], v) < 1e-4, k
+
+
+def test_determinism_bitwise():
+    """Fixed-order reductions: two identical train steps give identical bits."""
+    from unet_amd.model import UNetModel
+    rng = np.random.default_rng(3)
+    x, y = _data(rng, 4, 64, 64, 1)
+    outs = []
+    for _ in range(2):
+        m = UNetModel((64, 64, 3), 1, seed=5)
+        m.compile(None, "dice_loss")
+        m.train_step(x, y)
+        m.train_step(x, y)
+        torch.cuda.synchronize()
+        outs.append((m.engine.params.cpu().clone(), m.engine.stats.cpu().clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_full_size_train_steps_cfg2():
+    """configs[1] shape (256x256x3, batch 16): loss decreases on a fixed batch, no NaNs, and
+    size-independent properties hold (probabilities in [0,1], dice = 1 - loss)."""
+    from unet_amd.model import UNetModel
+    from unet_amd.metrics import MeanIoU
+    rng = np.random.default_rng(0)
+    x, y = _data(rng, 16, 256, 256, 1)
+    m = UNetModel((256, 256, 3), 1)
+    miou = MeanIoU(2)
+    from unet_amd.optim import AdamW
+    m.compile(AdamW(2e-3, 1e-4), "dice_loss", [miou, "dice_coef"])
+    losses = []
+    for _ in range(6):
+        r = m.train_step(x, y).cpu().numpy()
+        assert np.isfinite(r).all()
+        assert abs(r[0] + r[1] - 1) < 1e-6
+        losses.append(r[0])
+    assert losses[-1] < losses[0]
+    p = m.predict(x[:2])
+    assert p.min() >= 0 and p.max() <= 1
+    assert miou.confusion_matrix().sum() == 6 * 16 * 256 * 256
+
+
+def test_meaniou_metric_api():
+    from unet_amd.metrics import MeanIoU
+    from oracle import keras_ops as K
+    rng = np.random.default_rng(1)
+    yt = (rng.random((2, 16, 16, 1)) > 0.5).astype(np.float32)
+    yp = rng.random((2, 16, 16, 1)).astype(np.float32)
+    m = MeanIoU(2, threshold=0.5)
+    m.update_state(yt, yp)
+    cm = K.meaniou_confusion(yt, yp, 2, 0.5)
+    assert abs(m.result() - K.meaniou_result(cm)) < 1e-12
+    m2 = MeanIoU(2)  # training semantics: truncation of raw probabilities
+    m2.update_state(yt, yp)
+    assert abs(m2.result() - K.meaniou_result(K.meaniou_confusion(yt, yp, 2))) < 1e-12
+
+
+def test_reference_loss_api():
+    from utils.loss import dice_loss, iou_loss, jaccard_loss
+    from utils.metrics import dice_coef, iou_coef
+    from oracle import keras_ops as K
+    rng = np.random.default_rng(2)
+    yt = (rng.random((3, 8, 8, 2)) > 0.5).astype(np.float32)
+    yp = rng.random((3, 8, 8, 2)).astype(np.float32)
+    assert abs(float(dice_coef(yt, yp)) - K.dice_coef(f32(yt), f32(yp))) < 1e-6
+    assert abs(float(iou_coef(yt, yp)) - K.iou_coef(f32(yt), f32(yp))) < 1e-6
+    assert abs(float(dice_loss(yt, yp)) - K.dice_loss(f32(yt), f32(yp))) < 1e-6
+    assert abs(float(iou_loss(yt, yp)) - K.iou_loss(f32(yt), f32(yp))) < 1e-6
+    assert jaccard_loss is iou_loss

@@ -1,0 +1,302 @@
+"""Per-op parity of the HIP kernels (through the C-ABI) against the NumPy oracle (float64),
+on seeded inputs at small shapes, including tails (pixel counts that are not a multiple of
+the 128-row tile, 3-channel inputs, 3-channel outputs) and every activation-view mode."""
+import numpy as np
+import pytest
+
+from helpers import bn_affine, dev, f32, host, norm_err, rel_err, view_value
+from oracle import keras_ops as K
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from unet_amd import ops as O
+    return O
+
+
+def _mk_view(O, mode, t, drop_rate=0.0, drop_seed=0):
+    """t: dict of device tensors -> ops.View"""
+    if mode == 0:
+        v = O.View.plain(t["src0"])
+    elif mode == 1:
+        v = O.View.bnrelu(t["src0"], t["sc0"], t["sh0"])
+    elif mode == 2:
+        v = O.View.pool_bnrelu(t["src0"], t["sc0"], t["sh0"])
+    else:
+        v = O.View.concat(t["src0"], t["src1"], t["sc1"], t["sh1"])
+    return v.dropout(drop_rate, drop_seed) if drop_rate > 0 else v
+
+
+def _view_inputs(rng, mode, n, h, w, c0, c1=0):
+    """Returns (numpy dict, device dict) of the view sources for logical dims (n,h,w)."""
+    a = {}
+    if mode == 2:
+        a["src0"] = f32(rng.standard_normal((n, 2 * h, 2 * w, c0)))
+    else:
+        a["src0"] = f32(rng.standard_normal((n, h, w, c0)))
+    if mode in (1, 2):
+        a["sc0"], a["sh0"] = bn_affine(rng, c0)
+    if mode == 3:
+        a["src1"] = f32(rng.standard_normal((n, h, w, c1)))
+        a["sc1"], a["sh1"] = bn_affine(rng, c1)
+    return a, {k: dev(v) for k, v in a.items()}
+
+
+VIEW_CASES = [
+    # mode, n, h, w, c0, c1, drop
+    (0, 2, 9, 7, 3, 0, 0.0),      # image input: 3 channels, scalar path, ragged pixels
+    (0, 2, 16, 16, 16, 0, 0.0),
+    (1, 2, 12, 10, 32, 0, 0.0),
+    (2, 2, 8, 8, 16, 0, 0.0),
+    (3, 2, 8, 6, 16, 16, 0.0),
+    (3, 2, 8, 8, 8, 8, 0.2),      # decoder concat with dropout
+    (1, 1, 4, 4, 64, 0, 0.2),
+]
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,drop", VIEW_CASES)
+def test_view_materialize(ops, mode, n, h, w, c0, c1, drop):
+    rng = np.random.default_rng(10 + mode)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    v = _mk_view(ops, mode, t, drop, 1234)
+    out = torch.empty((n, h, w, c0 + c1), device="cuda")
+    ops.view_materialize(v, n, h, w, out)
+    ref = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"),
+                     drop, 1234)
+    assert rel_err(host(out), ref) < 1e-6
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,drop", VIEW_CASES)
+def test_dwconv_fwd(ops, mode, n, h, w, c0, c1, drop):
+    rng = np.random.default_rng(20 + mode)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = f32(rng.standard_normal((3, 3, C, 1)))
+    v = _mk_view(ops, mode, t, drop, 99)
+    y = torch.empty((n, h, w, C), device="cuda")
+    ops.dwconv3x3_fwd(v, n, h, w, dev(dk), y)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 99)
+    assert rel_err(host(y), K.depthwise3x3(xv, dk)) < 2e-6
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,drop", VIEW_CASES)
+def test_dwconv_bwd(ops, mode, n, h, w, c0, c1, drop):
+    rng = np.random.default_rng(30 + mode)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = f32(rng.standard_normal((3, 3, C, 1)))
+    dy = f32(rng.standard_normal((n, h, w, C)))
+    v = _mk_view(ops, mode, t, drop, 7)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 7)
+    dxv, ddk = K.depthwise3x3_bwd(xv, dk, dy)
+    if drop > 0:
+        dxv = dxv * K.dropout_mult(7, dxv.shape, drop)
+    # filter gradient
+    g = torch.empty((3, 3, C, 1), device="cuda")
+    ops.dwconv3x3_bwd_filter(v, n, h, w, dev(dy), g)
+    assert rel_err(host(g), ddk) < 1e-5
+    # data gradient, routed per view mode
+    if mode in (0, 1):
+        dx0 = torch.empty((n, h, w, C), device="cuda")
+        ops.dwconv3x3_bwd_data(v, n, h, w, dev(dk), dev(dy), dx0)
+        assert rel_err(host(dx0), dxv) < 2e-6
+    elif mode == 3:
+        dx0 = torch.empty((n, h, w, c0), device="cuda")
+        dx1 = torch.empty((n, h, w, c1), device="cuda")
+        ops.dwconv3x3_bwd_data(v, n, h, w, dev(dk), dev(dy), dx0, dx1)
+        assert rel_err(host(dx0), dxv[..., :c0]) < 2e-6
+        assert rel_err(host(dx1), dxv[..., c0:]) < 2e-6
+    else:
+        init = f32(rng.standard_normal((n, 2 * h, 2 * w, c0)))
+        dx0 = dev(init)
+        ops.dwconv3x3_bwd_data(v, n, h, w, dev(dk), dev(dy), dx0)
+        act = K.relu(a["src0"] * a["sc0"] + a["sh0"])
+        ref = init + K.maxpool2_bwd(act, dxv)
+        assert rel_err(host(dx0), ref) < 2e-6
+
+
+@pytest.mark.parametrize("m,cin,cout", [(100, 3, 64), (256, 64, 64), (300, 64, 128), (128, 128, 256),
+                                        (77, 32, 96), (512, 256, 512)])
+def test_pointwise_and_bn_stats(ops, m, cin, cout):
+    rng = np.random.default_rng(m + cin)
+    y = f32(rng.standard_normal((m, cin)))
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cin))
+    z = torch.empty((m, cout), device="cuda")
+    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    ops.pointwise_fwd(dev(y), m, cin, cout, dev(pk), z, part)
+    zr = y @ pk[0, 0]
+    assert rel_err(host(z), zr) < 5e-6
+    gamma, beta = bn_affine(rng, cout)
+    mm = f32(rng.standard_normal(cout) * 0.1)
+    mv = f32(1 + rng.random(cout))
+    tm, tv = dev(mm), dev(mv)
+    outs = [torch.empty(cout, device="cuda") for _ in range(4)]
+    ops.bn_finalize(part, m, cout, dev(gamma), dev(beta), 1e-3, 0.99, tm, tv, True, *outs)
+    zz = zr[:, None, None, :].reshape(m, 1, 1, cout)
+    out, mean, var = K.bn_train(zz, gamma, beta)
+    mm2, mv2 = K.bn_moving_update(mm, mv, mean, var)
+    inv = gamma / np.sqrt(var + 1e-3)
+    assert rel_err(host(outs[0]), mean) < 1e-4
+    assert rel_err(host(outs[1]), 1 / np.sqrt(var + 1e-3)) < 1e-5
+    assert rel_err(host(outs[2]), inv) < 1e-5
+    assert rel_err(host(outs[3]), beta - mean * inv) < 1e-4
+    assert rel_err(host(tm), mm2) < 1e-5 and rel_err(host(tv), mv2) < 1e-5
+    # no-partials path (inference GEMM epilogue)
+    z2 = torch.empty((m, cout), device="cuda")
+    ops.pointwise_fwd(dev(y), m, cin, cout, dev(pk), z2, None)
+    assert torch.equal(z, z2)
+
+
+@pytest.mark.parametrize("m,cin,cout", [(100, 3, 64), (256, 64, 64), (300, 128, 64), (200, 256, 512),
+                                        (64, 1024, 1024)])
+def test_pointwise_bwd(ops, m, cin, cout):
+    rng = np.random.default_rng(m * 3 + cout)
+    y = f32(rng.standard_normal((m, cin)))
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cin))
+    dz = f32(rng.standard_normal((m, cout)))
+    dy = torch.empty((m, cin), device="cuda")
+    ops.pointwise_bwd_data(dev(dz), m, cin, cout, dev(pk), dy)
+    dpk = torch.empty((1, 1, cin, cout), device="cuda")
+    ops.pointwise_bwd_filter(dev(y), dev(dz), m, cin, cout, dpk)
+    ry, rpk = K.pointwise_bwd(y.reshape(m, 1, 1, cin), pk, dz.reshape(m, 1, 1, cout))
+    assert rel_err(host(dy), ry.reshape(m, cin)) < 5e-6
+    assert rel_err(host(dpk), rpk) < 5e-6
+
+
+@pytest.mark.parametrize("use_bn,drop", [(True, 0.0), (True, 0.2), (False, 0.0)])
+@pytest.mark.parametrize("m,c", [(300, 16), (1000, 64), (96, 3)])
+def test_bn_relu_bwd(ops, use_bn, drop, m, c):
+    rng = np.random.default_rng(m + c)
+    z = f32(rng.standard_normal((m, 1, 1, c)) * 2 + 0.3)
+    da = f32(rng.standard_normal((m, 1, 1, c)))
+    gamma, beta = bn_affine(rng, c)
+    if use_bn:
+        _, mean, var = K.bn_train(z, gamma, beta)
+        rstd = 1 / np.sqrt(var + 1e-3)
+        scale = f32(gamma * rstd)
+        shift = f32(beta - mean * gamma * rstd)
+    else:
+        mean = var = rstd = np.zeros(c)
+        scale, shift = np.ones(c), beta
+    dmult = K.dropout_mult(55, da.shape, drop) if drop > 0 else None
+    dg = torch.zeros(c, device="cuda")
+    db = torch.zeros(c, device="cuda")
+    dz = torch.empty((m, c), device="cuda")
+    ops.bn_relu_bwd(dev(da), dev(z), m, c, dev(f32(mean)), dev(f32(rstd)), dev(scale), dev(shift), use_bn, drop, 55,
+                    dg if use_bn else None, db, dz)
+    if use_bn:
+        rz, rg, rb = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var), drop=dmult)
+        assert rel_err(host(dg), rg) < 1e-4
+    else:
+        g = da if dmult is None else da * dmult
+        rz = np.where(z + beta > 0, g, 0)
+        rb = rz.reshape(-1, c).sum(0)
+    assert rel_err(host(db), rb) < 1e-5
+    assert rel_err(host(dz), rz.reshape(m, c)) < 1e-4
+
+
+@pytest.mark.parametrize("mode,drop", [(1, 0.0), (1, 0.2), (0, 0.0)])
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 4, 4, 64, 32), (2, 3, 5, 32, 16), (1, 8, 8, 128, 64)])
+def test_conv_transpose(ops, mode, drop, n, h, w, cin, cout):
+    rng = np.random.default_rng(n * h * w + cin)
+    a, t = _view_inputs(rng, mode, n, h, w, cin)
+    v = _mk_view(ops, mode, t, drop, 4242)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), drop_rate=drop, drop_seed=4242)
+    k = f32(rng.standard_normal((2, 2, cout, cin)) / np.sqrt(cin))
+    b = f32(rng.standard_normal(cout))
+    out = torch.empty((n, 2 * h, 2 * w, cout), device="cuda")
+    ops.conv_transpose2x2_fwd(v, n, h, w, cout, dev(k), dev(b), out)
+    assert rel_err(host(out), K.conv_transpose2x2(xv, k, b)) < 5e-6
+    dout = f32(rng.standard_normal((n, 2 * h, 2 * w, cout)))
+    dx = torch.empty((n, h, w, cin), device="cuda")
+    dk = torch.empty((2, 2, cout, cin), device="cuda")
+    db = torch.empty(cout, device="cuda")
+    ops.conv_transpose2x2_bwd(v, n, h, w, cout, dev(k), dev(dout), dx, dk, db)
+    rdx, rdk, rdb = K.conv_transpose2x2_bwd(xv, k, dout)
+    assert rel_err(host(dx), rdx) < 5e-6
+    assert rel_err(host(dk), rdk) < 5e-6
+    assert rel_err(host(db), rdb) < 5e-6
+
+
+@pytest.mark.parametrize("ncls", [1, 21])
+@pytest.mark.parametrize("loss_kind", [0, 1])
+def test_head_dice(ops, ncls, loss_kind):
+    rng = np.random.default_rng(ncls + 7 * loss_kind)
+    n, h, w, cin = 2, 12, 10, 64
+    a, t = _view_inputs(rng, 1, n, h, w, cin)
+    v = _mk_view(ops, 1, t)
+    xv = view_value(1, a["src0"], a["sc0"], a["sh0"])
+    k = f32(rng.standard_normal((1, 1, cin, ncls)) * 0.2)
+    b = f32(rng.standard_normal(ncls) * 0.1)
+    prob = torch.empty((n, h, w, ncls), device="cuda")
+    ops.head_fwd(v, n, h, w, ncls, dev(k), dev(b), prob)
+    rp = K.head(xv, k, b, ncls)
+    assert rel_err(host(prob), rp) < 2e-6
+    if ncls == 1:
+        yt = (rng.random((n, h, w, 1)) > 0.5).astype(np.float64)
+    else:
+        cls = rng.integers(0, ncls, (n, h, w))
+        yt = np.eye(ncls)[cls]
+    sums = torch.empty(n * ncls * 3, device="cuda")
+    res = torch.empty(3, device="cuda")
+    ops.dice_fwd(dev(yt), prob, n, h * w, ncls, 1e-7, sums, res)
+    pp = host(prob)
+    r = host(res)
+    assert abs(r[0] - K.dice_loss(yt, pp)) < 1e-6
+    assert abs(r[1] - K.dice_coef(yt, pp)) < 1e-6
+    assert abs(r[2] - K.iou_coef(yt, pp)) < 1e-6
+    dx = torch.empty((n, h, w, cin), device="cuda")
+    dk = torch.empty((1, 1, cin, ncls), device="cuda")
+    db = torch.empty(ncls, device="cuda")
+    ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, loss_kind, dx, dk, db)
+    dprob = K.dice_loss_grad(yt, pp) if loss_kind == 0 else K.iou_loss_grad(yt, pp)
+    rdx, rdk, rdb = K.head_bwd(xv, k, pp, dprob, ncls)
+    assert rel_err(host(dx), rdx) < 1e-4
+    assert rel_err(host(dk), rdk) < 1e-4
+    assert rel_err(host(db), rdb) < 1e-4
+
+
+@pytest.mark.parametrize("ncls,thr", [(2, None), (2, 0.5), (5, None), (3, 0.3)])
+def test_meaniou(ops, ncls, thr):
+    rng = np.random.default_rng(ncls)
+    count = 100003
+    yt = rng.integers(0, ncls if thr is None else 2, count).astype(np.float64)
+    if thr is None:
+        yp = rng.random(count) * ncls
+        yp[::7] = np.floor(yp[::7])
+        yp[::11] = 1.0
+    else:
+        yp = rng.random(count)
+    conf = torch.zeros(ncls * ncls, dtype=torch.int64, device="cuda")
+    ops.meaniou_update(dev(yt), dev(yp), ncls, thr, conf)
+    ops.meaniou_update(dev(yt), dev(yp), ncls, thr, conf)  # accumulates
+    ref = 2 * K.meaniou_confusion(f32(yt), f32(yp), ncls, thr)
+    assert np.array_equal(conf.cpu().numpy().reshape(ncls, ncls), ref)
+
+
+def test_adamw(ops):
+    rng = np.random.default_rng(5)
+    n = 10007
+    p, g = f32(rng.standard_normal(n)), f32(rng.standard_normal(n) * 0.1)
+    m, v = f32(rng.standard_normal(n) * 0.01), f32(rng.random(n) * 0.01)
+    tp, tg, tm, tv = dev(p), dev(g), dev(m), dev(v)
+    step, lr, wd = 3, 2e-3, 1e-4
+    alpha = lr * np.sqrt(1 - 0.999 ** step) / (1 - 0.9 ** step)
+    ops.adamw_step(tp, tg, tm, tv, lr, wd, 0.9, 0.999, 1e-7, alpha, 0.5)
+    rp, rm, rv = K.adamw_update(p, g * 0.5, m, v, step, lr, wd)
+    assert rel_err(host(tp), rp) < 1e-6
+    assert rel_err(host(tm), rm) < 1e-6
+    assert rel_err(host(tv), rv) < 1e-6
+
+
+def test_errors_are_loud(ops):
+    from unet_amd._lib import UnetHipError
+    x = torch.zeros((1, 4, 4, 8), device="cuda")
+    with pytest.raises(UnetHipError):  # workspace / shape validation in the C-ABI
+        ops.dwconv3x3_fwd(ops.View(1, x, 8), 1, 4, 4, torch.zeros(72, device="cuda"), torch.empty_like(x))
+    with pytest.raises(ValueError):
+        ops.dwconv3x3_fwd(ops.View.plain(x.cpu()), 1, 4, 4, torch.zeros(72), torch.empty_like(x))

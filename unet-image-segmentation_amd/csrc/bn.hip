@@ -1,0 +1,376 @@
+// BatchNormalization + ReLU of conv_block (reference model/u_net.py:22-25; Keras 3
+// BatchNormalization defaults: momentum 0.99, epsilon 1e-3, batch statistics from
+// tf.nn.moments = biased variance, moving stats updated with the same biased variance).
+//
+// Forward statistics come from the pointwise-GEMM epilogue as per-128-row (mean, M2)
+// partials; unet_bn_finalize combines them with Chan's formula in double, in a fixed
+// order, and emits the folded affine (scale, shift) that activation views apply on load.
+// Backward is two passes over (da, z): per-channel sums (g, g*xhat) then the elementwise
+// dz, with the ReLU mask and the consumer's dropout mask recomputed, not stored.
+#include "view.h"
+
+namespace unet {
+
+namespace {
+constexpr int kStatsRows = 128;
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int64_t nblk, int64_t M,
+                                                          int C, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float momentum,
+                                                          float* moving_mean, float* moving_var, int update_moving,
+                                                          float* mean_out, float* rstd_out, float* scale_out,
+                                                          float* shift_out) {
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
+    Moments acc{0.0, 0.0, 0.0};
+    for (int64_t b = t; b < nblk; b += 256) {
+        const float2 pm = part[b * C + c];
+        const int64_t rows = (M - b * kStatsRows) < kStatsRows ? (M - b * kStatsRows) : kStatsRows;
+        acc = moments_combine(acc, Moments{(double)rows, (double)pm.x, (double)pm.y});
+    }
+    __shared__ double sn[256], smean[256], sm2[256];
+    sn[t] = acc.n;
+    smean[t] = acc.mean;
+    sm2[t] = acc.m2;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s) {
+            Moments a{sn[t], smean[t], sm2[t]}, b{sn[t + s], smean[t + s], sm2[t + s]};
+            Moments r = moments_combine(a, b);
+            sn[t] = r.n;
+            smean[t] = r.mean;
+            sm2[t] = r.m2;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float mean = (float)smean[0];
+        const float var = (float)(sm2[0] / (double)M);
+        const float rstd = 1.0f / sqrtf(var + eps);
+        if (gamma) {
+            const float sc = gamma[c] * rstd;
+            scale_out[c] = sc;
+            shift_out[c] = beta[c] - mean * sc;
+        } else {  // use_batch_norm=False: relu(z + bias)
+            scale_out[c] = 1.0f;
+            shift_out[c] = beta ? beta[c] : 0.f;
+        }
+        if (mean_out) mean_out[c] = mean;
+        if (rstd_out) rstd_out[c] = rstd;
+        if (update_moving && moving_mean && moving_var) {
+            moving_mean[c] = moving_mean[c] * momentum + mean * (1.0f - momentum);
+            moving_var[c] = moving_var[c] * momentum + var * (1.0f - momentum);
+        }
+    }
+}
+
+__global__ void bn_infer_kernel(const float* gamma, const float* beta, const float* mm, const float* mv, int C,
+                                float eps, float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (gamma) {
+        const float inv = 1.0f / sqrtf(mv[c] + eps);
+        const float sc = gamma[c] * inv;
+        scale[c] = sc;
+        shift[c] = beta[c] - mm[c] * sc;
+    } else {
+        scale[c] = 1.0f;
+        shift[c] = beta ? beta[c] : 0.f;
+    }
+}
+
+// Column-block x row-lane geometry shared by the reductions below: CT channel quads per
+// block, PL = 256/CT row lanes; rows [chunk * rpc, ...).
+struct RedPlan {
+    int ctiles, CT;
+    int64_t chunks, rpc;
+};
+RedPlan red_plan(int64_t rows, int cols) {
+    RedPlan p;
+    const int CQ = cols % 4 == 0 ? cols / 4 : cols;
+    p.CT = CQ < 64 ? CQ : 64;
+    p.ctiles = (int)cdiv(CQ, p.CT);
+    int64_t want = cdiv(2048, p.ctiles);
+    int64_t maxc = cdiv(rows, 128);
+    p.chunks = want < maxc ? want : maxc;
+    if (p.chunks < 1) p.chunks = 1;
+    p.rpc = cdiv(rows, p.chunks);
+    p.chunks = cdiv(rows, p.rpc);
+    return p;
+}
+
+// g = da * drop * [z*sc+sh > 0];  partial[chunk][0][c] = sum g, partial[chunk][1][c] = sum g*xhat
+template <bool DROP, bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                            int64_t M, int C, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            float rate, float inv_keep, uint64_t seed, int CT,
+                                                            int64_t rpc, float* __restrict__ part) {
+    const int CQ = VEC ? C / 4 : C;
+    const int PL = 256 / CT;
+    const int tid = threadIdx.x, cl = tid % CT, pl = tid / CT;
+    const int cq = blockIdx.x * CT + cl;
+    const int64_t r0 = (int64_t)blockIdx.y * rpc;
+    const int64_t r1 = r0 + rpc < M ? r0 + rpc : M;
+    __shared__ float4 red[2][256];
+    float4 sg = f4(0.f), sgx = f4(0.f);
+    if (pl < PL && cq < CQ) {
+        if constexpr (VEC) {
+            const int c = cq * 4;
+            const float4 s4 = ld4(sc + c), h4 = ld4(sh + c), mu = ld4(mean + c), rs = ld4(rstd + c);
+            for (int64_t m = r0 + pl; m < r1; m += PL) {
+                const float4 zz = ld4(z + m * C + c);
+                float4 g = ld4(da + m * C + c);
+                if constexpr (DROP) {
+                    const uint64_t i = (uint64_t)m * C + c;
+                    g.x *= drop_mult(seed, i + 0, rate, inv_keep);
+                    g.y *= drop_mult(seed, i + 1, rate, inv_keep);
+                    g.z *= drop_mult(seed, i + 2, rate, inv_keep);
+                    g.w *= drop_mult(seed, i + 3, rate, inv_keep);
+                }
+                g.x = fmaf(zz.x, s4.x, h4.x) > 0.f ? g.x : 0.f;
+                g.y = fmaf(zz.y, s4.y, h4.y) > 0.f ? g.y : 0.f;
+                g.z = fmaf(zz.z, s4.z, h4.z) > 0.f ? g.z : 0.f;
+                g.w = fmaf(zz.w, s4.w, h4.w) > 0.f ? g.w : 0.f;
+                sg = add4(sg, g);
+                float4 xh = make_float4((zz.x - mu.x) * rs.x, (zz.y - mu.y) * rs.y, (zz.z - mu.z) * rs.z,
+                                        (zz.w - mu.w) * rs.w);
+                sgx = fma4(g, xh, sgx);
+            }
+        } else {
+            const int c = cq;
+            const float s1 = sc[c], h1 = sh[c], mu = mean[c], rs = rstd[c];
+            for (int64_t m = r0 + pl; m < r1; m += PL) {
+                const float zz = z[m * C + c];
+                float g = da[m * C + c];
+                if constexpr (DROP) g *= drop_mult(seed, (uint64_t)m * C + c, rate, inv_keep);
+                g = fmaf(zz, s1, h1) > 0.f ? g : 0.f;
+                sg.x += g;
+                sgx.x = fmaf(g, (zz - mu) * rs, sgx.x);
+            }
+        }
+    }
+    red[0][tid] = sg;
+    red[1][tid] = sgx;
+    __syncthreads();
+    if (pl == 0 && cq < CQ) {
+        float4 a = red[0][cl], b = red[1][cl];
+        for (int q = 1; q < PL; ++q) {
+            a = add4(a, red[0][q * CT + cl]);
+            b = add4(b, red[1][q * CT + cl]);
+        }
+        float* out = part + (int64_t)blockIdx.y * 2 * C;
+        if constexpr (VEC) {
+            st4(out + cq * 4, a);
+            st4(out + C + cq * 4, b);
+        } else {
+            out[cq] = a.x;
+            out[C + cq] = b.x;
+        }
+    }
+}
+
+template <bool DROP, bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                           int64_t M, int C, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const float* __restrict__ sc, const float* __restrict__ sh,
+                                                           float rate, float inv_keep, uint64_t seed, int use_bn,
+                                                           const float* __restrict__ sums, float* __restrict__ dz) {
+    const int CQ = VEC ? C / 4 : C;
+    const int64_t total = M * CQ;
+    const float invM = 1.0f / (float)M;
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int cq = (int)(idx % CQ);
+        const int64_t m = idx / CQ;
+        if constexpr (VEC) {
+            const int c = cq * 4;
+            const float4 zz = ld4(z + m * C + c), s4 = ld4(sc + c), h4 = ld4(sh + c);
+            float4 g = ld4(da + m * C + c);
+            if constexpr (DROP) {
+                const uint64_t i = (uint64_t)m * C + c;
+                g.x *= drop_mult(seed, i + 0, rate, inv_keep);
+                g.y *= drop_mult(seed, i + 1, rate, inv_keep);
+                g.z *= drop_mult(seed, i + 2, rate, inv_keep);
+                g.w *= drop_mult(seed, i + 3, rate, inv_keep);
+            }
+            g.x = fmaf(zz.x, s4.x, h4.x) > 0.f ? g.x : 0.f;
+            g.y = fmaf(zz.y, s4.y, h4.y) > 0.f ? g.y : 0.f;
+            g.z = fmaf(zz.z, s4.z, h4.z) > 0.f ? g.z : 0.f;
+            g.w = fmaf(zz.w, s4.w, h4.w) > 0.f ? g.w : 0.f;
+            float4 o = g;
+            if (use_bn) {
+                const float4 mu = ld4(mean + c), rs = ld4(rstd + c);
+                const float4 sb = ld4(sums + c), sgx = ld4(sums + C + c);
+                o.x = s4.x * (g.x - sb.x * invM - (zz.x - mu.x) * rs.x * sgx.x * invM);
+                o.y = s4.y * (g.y - sb.y * invM - (zz.y - mu.y) * rs.y * sgx.y * invM);
+                o.z = s4.z * (g.z - sb.z * invM - (zz.z - mu.z) * rs.z * sgx.z * invM);
+                o.w = s4.w * (g.w - sb.w * invM - (zz.w - mu.w) * rs.w * sgx.w * invM);
+            }
+            st4(dz + m * C + c, o);
+        } else {
+            const int c = cq;
+            const float zz = z[m * C + c];
+            float g = da[m * C + c];
+            if constexpr (DROP) g *= drop_mult(seed, (uint64_t)m * C + c, rate, inv_keep);
+            g = fmaf(zz, sc[c], sh[c]) > 0.f ? g : 0.f;
+            float o = g;
+            if (use_bn) o = sc[c] * (g - sums[c] * invM - (zz - mean[c]) * rstd[c] * sums[C + c] * invM);
+            dz[m * C + c] = o;
+        }
+    }
+}
+
+// scatter the reduced sums: dbeta = sums[0], dgamma = sums[1]
+__global__ void bn_bwd_store_kernel(const float* sums, int C, int use_bn, float* dgamma, float* dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (dbeta) dbeta[c] = sums[c];
+    if (use_bn && dgamma) dgamma[c] = sums[C + c];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int64_t rows, int C, int CT,
+                                                     int64_t rpc, float* __restrict__ part) {
+    const int CQ = VEC ? C / 4 : C;
+    const int PL = 256 / CT;
+    const int tid = threadIdx.x, cl = tid % CT, pl = tid / CT;
+    const int cq = blockIdx.x * CT + cl;
+    const int64_t r0 = (int64_t)blockIdx.y * rpc;
+    const int64_t r1 = r0 + rpc < rows ? r0 + rpc : rows;
+    __shared__ float4 red[256];
+    float4 s = f4(0.f);
+    if (pl < PL && cq < CQ) {
+        if constexpr (VEC) {
+            for (int64_t m = r0 + pl; m < r1; m += PL) s = add4(s, ld4(x + m * C + cq * 4));
+        } else {
+            for (int64_t m = r0 + pl; m < r1; m += PL) s.x += x[m * C + cq];
+        }
+    }
+    red[tid] = s;
+    __syncthreads();
+    if (pl == 0 && cq < CQ) {
+        float4 a = red[cl];
+        for (int q = 1; q < PL; ++q) a = add4(a, red[q * CT + cl]);
+        float* out = part + (int64_t)blockIdx.y * C;
+        if constexpr (VEC)
+            st4(out + cq * 4, a);
+        else
+            out[cq] = a.x;
+    }
+}
+
+int grid_for(int64_t work) {
+    int64_t g = cdiv(work, 256);
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+}  // namespace
+
+size_t colsum_workspace(int64_t rows, int cols) {
+    RedPlan p = red_plan(rows, cols);
+    return align_up((size_t)p.chunks * cols * sizeof(float), 256);
+}
+
+int colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, hipStream_t st) {
+    RedPlan p = red_plan(rows, cols);
+    const size_t need = (size_t)p.chunks * cols * sizeof(float);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "colsum: workspace %zu < %zu", ws_bytes, need);
+    float* part = static_cast<float*>(ws);
+    dim3 grid(p.ctiles, (unsigned)p.chunks);
+    if (cols % 4 == 0)
+        colsum_kernel<true><<<grid, 256, 0, st>>>(x, rows, cols, p.CT, p.rpc, part);
+    else
+        colsum_kernel<false><<<grid, 256, 0, st>>>(x, rows, cols, p.CT, p.rpc, part);
+    UNET_CHECK_LAUNCH("colsum");
+    return reduce_slabs(part, (int)p.chunks, cols, out, cols, cols, st);
+}
+
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" int unet_bn_finalize(const float* bn_partials, int64_t m, int c, const float* gamma, const float* beta,
+                                float eps, float momentum, float* moving_mean, float* moving_var, int update_moving,
+                                float* mean, float* rstd, float* scale, float* shift, unet_stream_t stream) {
+    UNET_CHECK_ARG(bn_partials && scale && shift && m > 0 && c > 0, "unet_bn_finalize: bad args");
+    UNET_CHECK_ARG(!gamma || beta, "unet_bn_finalize: gamma without beta");
+    bn_finalize_kernel<<<c, 256, 0, as_stream(stream)>>>(reinterpret_cast<const float2*>(bn_partials),
+                                                         cdiv(m, kStatsRows), m, c, gamma, beta, eps, momentum,
+                                                         moving_mean, moving_var, update_moving, mean, rstd, scale,
+                                                         shift);
+    UNET_CHECK_LAUNCH("unet_bn_finalize");
+    return 0;
+}
+
+extern "C" int unet_bn_infer_params(const float* gamma, const float* beta, const float* moving_mean,
+                                    const float* moving_var, int c, float eps, float* scale, float* shift,
+                                    unet_stream_t stream) {
+    UNET_CHECK_ARG(scale && shift && c > 0, "unet_bn_infer_params: bad args");
+    UNET_CHECK_ARG(!gamma || (beta && moving_mean && moving_var), "unet_bn_infer_params: missing BN tensors");
+    bn_infer_kernel<<<(unsigned)cdiv(c, 256), 256, 0, as_stream(stream)>>>(gamma, beta, moving_mean, moving_var, c,
+                                                                           eps, scale, shift);
+    UNET_CHECK_LAUNCH("unet_bn_infer_params");
+    return 0;
+}
+
+extern "C" size_t unet_bn_relu_bwd_workspace(int64_t m, int c) {
+    if (m <= 0 || c <= 0) return 0;
+    RedPlan p = red_plan(m, c);
+    return align_up((size_t)p.chunks * 2 * c * sizeof(float), 256) + align_up((size_t)2 * c * sizeof(float), 256);
+}
+
+extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int c, const float* mean,
+                                const float* rstd, const float* scale, const float* shift, int use_bn,
+                                float drop_rate, uint64_t drop_seed, float* dgamma, float* dbeta, float* dz,
+                                void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(da && z && scale && shift && dz && m > 0 && c > 0, "unet_bn_relu_bwd: bad args");
+    UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_relu_bwd: use_bn needs mean/rstd");
+    UNET_CHECK_ARG(drop_rate >= 0.f && drop_rate < 1.f, "unet_bn_relu_bwd: bad drop_rate");
+    const size_t need = unet_bn_relu_bwd_workspace(m, c);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_bn_relu_bwd: workspace %zu < %zu", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    RedPlan p = red_plan(m, c);
+    float* part = static_cast<float*>(ws);
+    float* sums = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                           align_up((size_t)p.chunks * 2 * c * sizeof(float), 256));
+    const float* mu = use_bn ? mean : scale;  // unused when !use_bn (mask only)
+    const float* rs = use_bn ? rstd : scale;
+    const float inv_keep = drop_rate > 0.f ? 1.0f / (1.0f - drop_rate) : 1.0f;
+    const bool vec = c % 4 == 0;
+    const bool drop = drop_rate > 0.f;
+    dim3 grid(p.ctiles, (unsigned)p.chunks);
+#define UNET_BNB(D, V)                                                                                        \
+    bn_bwd_reduce_kernel<D, V><<<grid, 256, 0, st>>>(da, z, m, c, mu, rs, scale, shift, drop_rate, inv_keep, \
+                                                     drop_seed, p.CT, p.rpc, part)
+    if (drop) {
+        if (vec) UNET_BNB(true, true);
+        else UNET_BNB(true, false);
+    } else {
+        if (vec) UNET_BNB(false, true);
+        else UNET_BNB(false, false);
+    }
+#undef UNET_BNB
+    UNET_CHECK_LAUNCH("unet_bn_relu_bwd(reduce)");
+    int rc = reduce_slabs(part, (int)p.chunks, (int64_t)2 * c, sums, (int64_t)2 * c, (int64_t)2 * c, st);
+    if (rc) return rc;
+    bn_bwd_store_kernel<<<(unsigned)cdiv(c, 256), 256, 0, st>>>(sums, c, use_bn, dgamma, dbeta);
+    UNET_CHECK_LAUNCH("unet_bn_relu_bwd(store)");
+    const int64_t work = m * (vec ? c / 4 : c);
+    const int g2 = grid_for(work);
+#define UNET_BNA(D, V)                                                                                             \
+    bn_bwd_apply_kernel<D, V><<<g2, 256, 0, st>>>(da, z, m, c, mu, rs, scale, shift, drop_rate, inv_keep, drop_seed, \
+                                                  use_bn, sums, dz)
+    if (drop) {
+        if (vec) UNET_BNA(true, true);
+        else UNET_BNA(true, false);
+    } else {
+        if (vec) UNET_BNA(false, true);
+        else UNET_BNA(false, false);
+    }
+#undef UNET_BNA
+    UNET_CHECK_LAUNCH("unet_bn_relu_bwd(apply)");
+    return 0;
+}

@@ -1,0 +1,111 @@
+// Shared device helpers for libunet_hip.so (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/unet_hip.h"
+
+namespace unet {
+
+// ---------------------------------------------------------------- errors ----
+void set_error(const char* fmt, ...);
+
+#define UNET_CHECK_ARG(cond, ...)        \
+    do {                                 \
+        if (!(cond)) {                   \
+            ::unet::set_error(__VA_ARGS__); \
+            return -1;                   \
+        }                                \
+    } while (0)
+
+#define UNET_CHECK_LAUNCH(what)                                          \
+    do {                                                                 \
+        hipError_t e_ = hipGetLastError();                               \
+        if (e_ != hipSuccess) {                                          \
+            ::unet::set_error("%s: %s", what, hipGetErrorString(e_));     \
+            return (int)e_;                                              \
+        }                                                                \
+    } while (0)
+
+inline hipStream_t as_stream(unet_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// -------------------------------------------------------------- vectors ----
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 mul4(float4 a, float4 b) {
+    return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+__device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
+    return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z),
+                       fmaf(a.w, b.w, c.w));
+}
+__device__ __forceinline__ float4 max4(float4 a, float4 b) {
+    return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+}
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+__device__ __forceinline__ float4 relu4(float4 v) {
+    return make_float4(relu(v.x), relu(v.y), relu(v.z), relu(v.w));
+}
+// BatchNorm affine + ReLU as tf.nn.batch_normalization folds it: x*inv + (beta - mean*inv)
+__device__ __forceinline__ float bnrelu(float x, float sc, float sh) { return relu(fmaf(x, sc, sh)); }
+__device__ __forceinline__ float4 bnrelu4(float4 x, float4 sc, float4 sh) { return relu4(fma4(x, sc, sh)); }
+
+// --------------------------------------------------------------- dropout ----
+// keep(i) <=> u(i) >= rate, u(i) = top 24 bits of splitmix64(seed + i*golden) / 2^24.
+// The oracle restates this bit-for-bit (oracle/keras_ops.py: dropout_keep).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float drop_mult(uint64_t seed, uint64_t idx, float rate, float inv_keep) {
+    uint64_t h = splitmix64(seed + idx * 0x9E3779B97F4A7C15ull);
+    float u = (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f);
+    return u >= rate ? inv_keep : 0.f;
+}
+
+// ------------------------------------------------------------ reductions ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Chan et al. parallel combination of (count, mean, M2) in double.
+struct Moments {
+    double n, mean, m2;
+};
+__device__ __forceinline__ Moments moments_combine(Moments a, Moments b) {
+    if (b.n == 0.0) return a;
+    if (a.n == 0.0) return b;
+    double n = a.n + b.n;
+    double d = b.mean - a.mean;
+    Moments r;
+    r.n = n;
+    r.mean = a.mean + d * (b.n / n);
+    r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+    return r;
+}
+
+// ------------------------------------------------------------- host side ----
+// Deterministic ordered reduction of S slabs of L floats: out[l] = sum_s part[s*L + l]
+// (double accumulation, fixed order).  out has row stride ld_out for rows of `row`
+// floats (row == L, ld_out == L for a flat copy).
+int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out,
+                 hipStream_t stream);
+
+}  // namespace unet

@@ -1,0 +1,680 @@
+// FP32 MFMA GEMMs for the dense parts of the U-Net hot path (gfx950, v_mfma_f32_32x32x2_f32,
+// exact f32: a k-ordered fmaf chain per output).
+//
+//   gemm_rows  : C[M, N] = A[M, K] . B[K, N]   rows = pixels (NHWC), B = a small weight matrix
+//                  - pointwise half of SeparableConv2D fwd (model/u_net.py:14-20) with a
+//                    BatchNorm-statistics epilogue (u_net.py:22-23),
+//                  - its data gradient,
+//                  - Conv2DTranspose(2, stride 2) fwd (u_net.py:88-94) as [M, Cin] x [Cin, 4 Cout]
+//                    with a pixel-shuffle + bias epilogue (non-overlapping 2x2 taps),
+//                  - Conv2DTranspose data gradient (pixel-unshuffle A operand).
+//   gemm_wgrad : C[P, Q] = sum_m A[m, P] . B[m, Q]  (weight gradients, reduction over pixels),
+//                split over m into slices; slices are summed in a fixed order (reduce_slabs),
+//                so results are bitwise reproducible.
+//
+// Tiling (both kernels): 256 threads = 2x2 waves; each wave owns a (BM/2)x(BN/2) block of
+// 32x32 MFMA tiles.  Operands are staged global -> registers -> LDS (k-major [BK][rows+4]
+// images, so each MFMA operand fetch is one conflict-free ds_read_b32 per lane), double
+// buffered: the next stage's global loads are in flight while the current stage's MFMAs run.
+// The A operand passes through an activation view (BN+ReLU / dropout / unshuffle) on load.
+#include "view.h"
+
+namespace unet {
+
+int colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, hipStream_t st);
+size_t colsum_workspace(int64_t rows, int cols);
+
+namespace {
+
+constexpr int BK = 16;
+constexpr int kStatsRows = 128;  // rows per BatchNorm partial (= BM of the stats GEMM)
+
+enum { A_PLAIN = 0, A_BNRELU = 1, A_UNSHUFFLE = 2 };
+enum { E_STORE = 0, E_STATS = 1, E_SHUFFLE = 2 };
+
+struct RowsArgs {
+    DView a;  // A operand: PLAIN/BNRELU -> a.src0[m * a.c0 + k]; UNSHUFFLE -> a.src0 = dU
+    int64_t M;
+    int K;
+    int uH, uW, uf;  // UNSHUFFLE: m = (n, i, j) over uH x uW, dU is (n, 2uH, 2uW, uf)
+    const float* B;
+    int64_t sbk, sbn;
+    int N;
+    float* C;
+    int64_t ldc;
+    const float* bias;
+    float2* stats;
+    int sH, sW, sf;  // SHUFFLE epilogue: m = (n, i, j) over sH x sW, out (n, 2sH, 2sW, sf)
+};
+
+__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+template <int BM, int BN, int AMODE, bool DROP, int EPI>
+__global__ __launch_bounds__(256) void gemm_rows_kernel(RowsArgs g) {
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int AR = BM / 16;  // A elements per thread per stage
+    constexpr int BR = BN / 16;  // B elements per thread per stage
+    __shared__ float As[2][BK][LDA];
+    __shared__ float Bs[2][BK][LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int M_rem = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+
+    // ---- A staging geometry: k-lane ak, rows arow0 + 16 r
+    const int ak = tid & 15;
+    const int arow0 = tid >> 4;
+    int aoff[AR];
+#pragma unroll
+    for (int r = 0; r < AR; ++r) {
+        const int rr = arow0 + 16 * r;
+        if (rr < M_rem) {
+            const int64_t m = m0 + rr;
+            if constexpr (AMODE == A_UNSHUFFLE) {
+                const int64_t hw = (int64_t)g.uH * g.uW;
+                const int n = (int)(m / hw);
+                const int rem = (int)(m - (int64_t)n * hw);
+                const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
+                aoff[r] = ((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf;
+            } else {
+                aoff[r] = (int)(m * g.a.c0);
+            }
+        } else {
+            aoff[r] = -1;
+        }
+    }
+    // ---- B staging geometry
+    const bool bkc = g.sbk == 1;
+    int bk_[BR], bn_[BR];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+        if (bkc) {
+            bk_[r] = tid & 15;
+            bn_[r] = (tid >> 4) + 16 * r;
+        } else {
+            bn_[r] = tid % BN;
+            bk_[r] = tid / BN + (256 / BN) * r;
+        }
+    }
+
+    float ra[AR], rb[BR];
+    auto load_stage = [&](int k0) {
+        const int k = k0 + ak;
+        const bool kv = k < g.K;
+        int koff = k;
+        float sc = 1.f, sh = 0.f;
+        if constexpr (AMODE == A_UNSHUFFLE) {
+            const int ab = k / g.uf;
+            const int co = k - ab * g.uf;
+            koff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
+        }
+        if constexpr (AMODE == A_BNRELU) {
+            if (kv) {
+                sc = g.a.sc0[k];
+                sh = g.a.sh0[k];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < AR; ++r) {
+            float v = 0.f;
+            if (kv && aoff[r] >= 0) {
+                v = g.a.src0[aoff[r] + koff];
+                if constexpr (AMODE == A_BNRELU) v = bnrelu(v, sc, sh);
+                if constexpr (DROP)
+                    v *= drop_mult(g.a.seed, (uint64_t)(m0 + arow0 + 16 * r) * g.a.C + k, g.a.rate, g.a.inv_keep);
+            }
+            ra[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+            const int kk = k0 + bk_[r], nn = n0 + bn_[r];
+            rb[r] = (kk < g.K && nn < g.N) ? g.B[kk * g.sbk + nn * g.sbn] : 0.f;
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) As[buf][ak][arow0 + 16 * r] = ra[r];
+#pragma unroll
+        for (int r = 0; r < BR; ++r) Bs[buf][bk_[r]][bn_[r]] = rb[r];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+    const int nk = (g.K + BK - 1) / BK;
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage((kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) av[tm] = As[buf][2 * kk + hi][wm * (BM / 2) + tm * 32 + lo];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bv[tn] = Bs[buf][2 * kk + hi][wn * (BN / 2) + tn * 32 + lo];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---------------------------------------------------------------- epilogue
+    if constexpr (EPI == E_STORE || EPI == E_STATS) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
+                if (n >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
+                    if (rr < M_rem) g.C[(m0 + rr) * g.ldc + n] = acc[tm][tn][r];
+                }
+            }
+    }
+    if constexpr (EPI == E_STATS) {
+        // per-column (count, mean, M2) over this block's valid rows: two passes in registers
+        float* red = &As[0][0][0];
+        float mean[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            float s = 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) s += acc[tm][tn][r];
+            s += __shfl_xor(s, 32, 64);
+            if (hi == 0) red[wm * BN + col] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            mean[tn] = (red[col] + red[BN + col]) / (float)M_rem;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            float q = 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) {
+                        const float d = acc[tm][tn][r] - mean[tn];
+                        q = fmaf(d, d, q);
+                    }
+            q += __shfl_xor(q, 32, 64);
+            if (hi == 0) red[wm * BN + col] = q;
+        }
+        __syncthreads();
+        if (wm == 0 && hi == 0) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * (BN / 2) + tn * 32 + lo;
+                const int n = n0 + col;
+                if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = make_float2(mean[tn], red[col] + red[BN + col]);
+            }
+        }
+    }
+    if constexpr (EPI == E_SHUFFLE) {
+        const int64_t hw = (int64_t)g.sH * g.sW;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
+            if (n >= g.N) continue;
+            const int ab = n / g.sf;
+            const int co = n - ab * g.sf;
+            const int a = ab >> 1, b = ab & 1;
+            const float bias = g.bias ? g.bias[co] : 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
+                    if (rr >= M_rem) continue;
+                    const int64_t m = m0 + rr;
+                    const int img = (int)(m / hw);
+                    const int rem = (int)(m - img * hw);
+                    const int i = rem / g.sW, j = rem - (rem / g.sW) * g.sW;
+                    const int64_t o = ((int64_t)(img * 2 * g.sH + 2 * i + a) * (2 * g.sW) + 2 * j + b) * g.sf + co;
+                    g.C[o] = acc[tm][tn][r] + bias;
+                }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------- wgrad ----
+enum { W_PLAIN = 0, W_BNRELU = 1, W_UNSHUFFLE = 2 };
+
+struct WgradArgs {
+    DView a;
+    int P;
+    int uH, uW, uf;  // A UNSHUFFLE geometry (m over uH x uW, dU (n, 2uH, 2uW, uf))
+    DView b;
+    int Q;
+    int64_t M, mslice;
+    float* slab;  // [S][P][Q]
+};
+
+template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
+__global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
+    constexpr int LDA = BP + 4, LDB = BQ + 4;
+    constexpr int TM = BP / 64, TN = BQ / 64;
+    constexpr int AR = BP / 16, BR = BQ / 16;
+    constexpr int AS = 256 / BP, BS = 256 / BQ;  // row steps between a thread's staged elements
+    __shared__ float As[2][BK][LDA];
+    __shared__ float Bs[2][BK][LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wp = wave >> 1, wq = wave & 1;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int ntp = (g.P + BP - 1) / BP;
+    const int p0 = (blockIdx.x % ntp) * BP;
+    const int q0 = (blockIdx.x / ntp) * BQ;
+    const int64_t mb = (int64_t)blockIdx.y * g.mslice;
+    const int64_t me = mb + g.mslice < g.M ? mb + g.mslice : g.M;
+
+    // A: this thread stages column p = p0 + ap, rows amm + AS*r of each stage
+    const int ap = tid % BP, amm = tid / BP;
+    const int p = p0 + ap;
+    const bool pv = p < g.P;
+    float asc = 1.f, ash = 0.f;
+    int poff = p;
+    if constexpr (AMODE == W_BNRELU) {
+        if (pv) {
+            asc = g.a.sc0[p];
+            ash = g.a.sh0[p];
+        }
+    }
+    if constexpr (AMODE == W_UNSHUFFLE) {
+        const int ab = p / g.uf;
+        const int co = p - ab * g.uf;
+        poff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
+    }
+    const int bq = tid % BQ, bmm = tid / BQ;
+    const int q = q0 + bq;
+    const bool qv = q < g.Q;
+    float bsc = 1.f, bsh = 0.f;
+    if constexpr (BMODE == W_BNRELU) {
+        if (qv) {
+            bsc = g.b.sc0[q];
+            bsh = g.b.sh0[q];
+        }
+    }
+
+    float ra[AR], rb[BR];
+    auto load_stage = [&](int64_t k0) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) {
+            const int64_t m = k0 + amm + AS * r;
+            float v = 0.f;
+            if (pv && m < me) {
+                if constexpr (AMODE == W_UNSHUFFLE) {
+                    const int64_t hw = (int64_t)g.uH * g.uW;
+                    const int n = (int)(m / hw);
+                    const int rem = (int)(m - n * hw);
+                    const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
+                    v = g.a.src0[(int64_t)((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf + poff];
+                } else {
+                    v = g.a.src0[m * g.a.c0 + p];
+                    if constexpr (AMODE == W_BNRELU) v = bnrelu(v, asc, ash);
+                    if constexpr (ADROP) v *= drop_mult(g.a.seed, (uint64_t)m * g.a.C + p, g.a.rate, g.a.inv_keep);
+                }
+            }
+            ra[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+            const int64_t m = k0 + bmm + BS * r;
+            float v = 0.f;
+            if (qv && m < me) {
+                v = g.b.src0[m * g.b.c0 + q];
+                if constexpr (BMODE == W_BNRELU) v = bnrelu(v, bsc, bsh);
+                if constexpr (BDROP) v *= drop_mult(g.b.seed, (uint64_t)m * g.b.C + q, g.b.rate, g.b.inv_keep);
+            }
+            rb[r] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) As[buf][amm + AS * r][ap] = ra[r];
+#pragma unroll
+        for (int r = 0; r < BR; ++r) Bs[buf][bmm + BS * r][bq] = rb[r];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+    const int nk = (int)((me - mb + BK - 1) / BK);
+    if (nk > 0) {
+        load_stage(mb);
+        store_stage(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage(mb + (int64_t)(kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) av[tm] = As[buf][2 * kk + hi][wp * (BP / 2) + tm * 32 + lo];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bv[tn] = Bs[buf][2 * kk + hi][wq * (BQ / 2) + tn * 32 + lo];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+    float* slab = g.slab + (int64_t)blockIdx.y * g.P * g.Q;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int qq = q0 + wq * (BQ / 2) + tn * 32 + lo;
+            if (qq >= g.Q) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pp = p0 + wp * (BP / 2) + tm * 32 + acc_row(r, hi);
+                if (pp < g.P) slab[(int64_t)pp * g.Q + qq] = acc[tm][tn][r];
+            }
+        }
+}
+
+// ------------------------------------------------------------------------------ launchers ----
+template <int AMODE, bool DROP, int EPI>
+int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
+    const unsigned gm = (unsigned)cdiv(a.M, 128);
+    if (a.N <= 64) {
+        dim3 grid(gm, (unsigned)cdiv(a.N, 64));
+        gemm_rows_kernel<128, 64, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+    } else {
+        dim3 grid(gm, (unsigned)cdiv(a.N, 128));
+        gemm_rows_kernel<128, 128, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+    }
+    UNET_CHECK_LAUNCH(what);
+    return 0;
+}
+
+struct WgradPlan {
+    int bp, bq, tiles, S;
+    int64_t mslice;
+};
+WgradPlan wgrad_plan(int64_t M, int P, int Q) {
+    WgradPlan w;
+    w.bp = P > 64 ? 128 : 64;
+    w.bq = Q > 64 ? 128 : 64;
+    w.tiles = (int)(cdiv(P, w.bp) * cdiv(Q, w.bq));
+    int64_t want = cdiv(2048, w.tiles);
+    int64_t maxs = M / 256;
+    if (maxs < 1) maxs = 1;
+    int64_t S = want < maxs ? want : maxs;
+    if (S < 1) S = 1;
+    w.mslice = cdiv(cdiv(M, S), BK) * BK;
+    w.S = (int)cdiv(M, w.mslice);
+    return w;
+}
+
+template <int AMODE, bool ADROP, int BMODE, bool BDROP>
+void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
+    dim3 grid((unsigned)w.tiles, (unsigned)w.S);
+    if (w.bp == 128 && w.bq == 128)
+        gemm_wgrad_kernel<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+    else if (w.bp == 128)
+        gemm_wgrad_kernel<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+    else if (w.bq == 128)
+        gemm_wgrad_kernel<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+    else
+        gemm_wgrad_kernel<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+}
+
+// out[P][Q] (row stride ldo) = sum_m A(m, p) B(m, q)
+int run_wgrad(WgradArgs a, int amode, int bmode, float* out, void* ws, size_t ws_bytes, hipStream_t st,
+              const char* what) {
+    WgradPlan w = wgrad_plan(a.M, a.P, a.Q);
+    const size_t need = (size_t)w.S * a.P * a.Q * sizeof(float);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", what, ws_bytes, need);
+    a.mslice = w.mslice;
+    a.slab = static_cast<float*>(ws);
+    const bool ad = a.a.rate > 0.f, bd = a.b.rate > 0.f;
+    if (amode == W_PLAIN && bmode == W_PLAIN) {
+        launch_wgrad_t<W_PLAIN, false, W_PLAIN, false>(a, w, st);
+    } else if (amode == W_UNSHUFFLE && bmode == W_BNRELU) {
+        if (bd)
+            launch_wgrad_t<W_UNSHUFFLE, false, W_BNRELU, true>(a, w, st);
+        else
+            launch_wgrad_t<W_UNSHUFFLE, false, W_BNRELU, false>(a, w, st);
+    } else if (amode == W_UNSHUFFLE && bmode == W_PLAIN) {
+        if (bd)
+            launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, true>(a, w, st);
+        else
+            launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, false>(a, w, st);
+    } else if (amode == W_BNRELU && bmode == W_PLAIN) {
+        if (ad)
+            launch_wgrad_t<W_BNRELU, true, W_PLAIN, false>(a, w, st);
+        else
+            launch_wgrad_t<W_BNRELU, false, W_PLAIN, false>(a, w, st);
+    } else {
+        UNET_CHECK_ARG(false, "%s: unsupported wgrad operand modes %d/%d", what, amode, bmode);
+    }
+    UNET_CHECK_LAUNCH(what);
+    return reduce_slabs(a.slab, w.S, (int64_t)a.P * a.Q, out, (int64_t)a.P * a.Q, (int64_t)a.P * a.Q, st);
+}
+
+size_t wgrad_workspace(int64_t M, int P, int Q) {
+    WgradPlan w = wgrad_plan(M, P, Q);
+    return align_up((size_t)w.S * P * Q * sizeof(float), 256);
+}
+
+DView plain_view(const float* p, int c) {
+    unet_view v{};
+    v.mode = UNET_VIEW_PLAIN;
+    v.c0 = c;
+    v.src0 = p;
+    return make_dview(v);
+}
+
+bool fits_i32(int64_t a, int64_t b) { return a * b < (int64_t(1) << 31); }
+
+}  // namespace
+}  // namespace unet
+
+using namespace unet;
+
+// ------------------------------------------------------------------- pointwise conv ----
+extern "C" size_t unet_bn_partials_size(int64_t m, int c) {
+    if (m <= 0 || c <= 0) return 0;
+    return (size_t)cdiv(m, kStatsRows) * c * sizeof(float2);
+}
+
+extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, const float* pw_kernel, float* z,
+                                  float* bn_partials, unet_stream_t stream) {
+    UNET_CHECK_ARG(y && pw_kernel && z, "unet_pointwise_fwd: null pointer");
+    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_fwd: bad sizes");
+    UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_fwd: tensor too large");
+    RowsArgs a{};
+    a.a = plain_view(y, cin);
+    a.M = m;
+    a.K = cin;
+    a.B = pw_kernel;
+    a.sbk = cout;
+    a.sbn = 1;
+    a.N = cout;
+    a.C = z;
+    a.ldc = cout;
+    a.stats = reinterpret_cast<float2*>(bn_partials);
+    hipStream_t st = as_stream(stream);
+    if (bn_partials) return launch_rows<A_PLAIN, false, E_STATS>(a, st, "unet_pointwise_fwd");
+    return launch_rows<A_PLAIN, false, E_STORE>(a, st, "unet_pointwise_fwd");
+}
+
+extern "C" int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout, const float* pw_kernel,
+                                       float* dy, unet_stream_t stream) {
+    UNET_CHECK_ARG(dz && pw_kernel && dy, "unet_pointwise_bwd_data: null pointer");
+    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_data: bad sizes");
+    UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_bwd_data: tensor too large");
+    RowsArgs a{};
+    a.a = plain_view(dz, cout);
+    a.M = m;
+    a.K = cout;
+    a.B = pw_kernel;  // B(k = co, n = ci) = k[ci][co]
+    a.sbk = 1;
+    a.sbn = cout;
+    a.N = cin;
+    a.C = dy;
+    a.ldc = cin;
+    return launch_rows<A_PLAIN, false, E_STORE>(a, as_stream(stream), "unet_pointwise_bwd_data");
+}
+
+extern "C" size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout) {
+    if (m <= 0 || cin <= 0 || cout <= 0) return 0;
+    return wgrad_workspace(m, cin, cout);
+}
+
+extern "C" int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m, int cin, int cout,
+                                         float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(y && dz && d_pw_kernel, "unet_pointwise_bwd_filter: null pointer");
+    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_filter: bad sizes");
+    WgradArgs a{};
+    a.a = plain_view(y, cin);
+    a.P = cin;
+    a.b = plain_view(dz, cout);
+    a.Q = cout;
+    a.M = m;
+    return run_wgrad(a, W_PLAIN, W_PLAIN, d_pw_kernel, ws, ws_bytes, as_stream(stream), "unet_pointwise_bwd_filter");
+}
+
+// ------------------------------------------------------------ transposed conv 2x2/2 ----
+extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
+                                          const float* bias, float* out, unet_stream_t stream) {
+    if (check_view(x, "unet_conv_transpose2x2_fwd")) return -1;
+    UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
+                   "unet_conv_transpose2x2_fwd: input view must be PLAIN or BNRELU");
+    UNET_CHECK_ARG(kernel && out && n > 0 && h > 0 && w > 0 && cout > 0, "unet_conv_transpose2x2_fwd: bad args");
+    const int cin = x->c0;
+    const int64_t M = (int64_t)n * h * w;
+    UNET_CHECK_ARG(fits_i32(M, cin) && fits_i32(4 * M, cout), "unet_conv_transpose2x2_fwd: tensor too large");
+    RowsArgs a{};
+    a.a = make_dview(*x);
+    a.M = M;
+    a.K = cin;
+    a.B = kernel;  // B(k = ci, n = (a, b, co)) = k[(a*2+b)*cout + co][ci]
+    a.sbk = 1;
+    a.sbn = cin;
+    a.N = 4 * cout;
+    a.C = out;
+    a.bias = bias;
+    a.sH = h;
+    a.sW = w;
+    a.sf = cout;
+    hipStream_t st = as_stream(stream);
+    const bool drop = x->drop_rate > 0.f;
+    if (x->mode == UNET_VIEW_PLAIN) {
+        if (drop) return launch_rows<A_PLAIN, true, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
+        return launch_rows<A_PLAIN, false, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
+    }
+    if (drop) return launch_rows<A_BNRELU, true, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
+    return launch_rows<A_BNRELU, false, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
+}
+
+extern "C" size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int cin, int cout) {
+    if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return 0;
+    const int64_t M = (int64_t)n * h * w;
+    size_t a = wgrad_workspace(M, 4 * cout, cin);
+    size_t b = colsum_workspace(4 * M, cout);
+    return a > b ? a : b;
+}
+
+extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
+                                          const float* dout, float* dx, float* dkernel, float* dbias, void* ws,
+                                          size_t ws_bytes, unet_stream_t stream) {
+    if (check_view(x, "unet_conv_transpose2x2_bwd")) return -1;
+    UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
+                   "unet_conv_transpose2x2_bwd: input view must be PLAIN or BNRELU");
+    UNET_CHECK_ARG(kernel && dout && dkernel && dbias && n > 0 && h > 0 && w > 0 && cout > 0,
+                   "unet_conv_transpose2x2_bwd: bad args");
+    const int cin = x->c0;
+    const int64_t M = (int64_t)n * h * w;
+    UNET_CHECK_ARG(fits_i32(M, cin) && fits_i32(4 * M, cout), "unet_conv_transpose2x2_bwd: tensor too large");
+    hipStream_t st = as_stream(stream);
+    const size_t need = unet_conv_transpose2x2_bwd_workspace(n, h, w, cin, cout);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_conv_transpose2x2_bwd: workspace %zu < %zu", ws_bytes, need);
+    // data gradient w.r.t. the view output: dx[m, ci] = sum_{(a,b,co)} dU'[m, (a,b,co)] k[(a,b,co)][ci]
+    if (dx) {
+        RowsArgs a{};
+        a.a = plain_view(dout, cout);
+        a.M = M;
+        a.K = 4 * cout;
+        a.uH = h;
+        a.uW = w;
+        a.uf = cout;
+        a.B = kernel;
+        a.sbk = cin;
+        a.sbn = 1;
+        a.N = cin;
+        a.C = dx;
+        a.ldc = cin;
+        int rc = launch_rows<A_UNSHUFFLE, false, E_STORE>(a, st, "unet_conv_transpose2x2_bwd(data)");
+        if (rc) return rc;
+    }
+    // kernel gradient: dk[(a,b,co)][ci] = sum_m dU'[m, (a,b,co)] x[m, ci]
+    WgradArgs wa{};
+    wa.a = plain_view(dout, cout);
+    wa.P = 4 * cout;
+    wa.uH = h;
+    wa.uW = w;
+    wa.uf = cout;
+    wa.b = make_dview(*x);
+    wa.Q = cin;
+    wa.M = M;
+    int rc = run_wgrad(wa, W_UNSHUFFLE, x->mode == UNET_VIEW_BNRELU ? W_BNRELU : W_PLAIN, dkernel, ws, ws_bytes, st,
+                       "unet_conv_transpose2x2_bwd(filter)");
+    if (rc) return rc;
+    return colsum(dout, 4 * M, cout, dbias, ws, ws_bytes, st);
+}
+
+namespace unet {
+// head dW = sum_m x(m, k) dlogit(m, c): used by head.hip
+int head_wgrad(const unet_view* x, int64_t M, const float* dlogit, int ncls, float* dkernel, void* ws, size_t ws_bytes,
+               hipStream_t st) {
+    WgradArgs a{};
+    a.a = make_dview(*x);
+    a.P = x->c0;
+    a.b = plain_view(dlogit, ncls);
+    a.Q = ncls;
+    a.M = M;
+    return run_wgrad(a, x->mode == UNET_VIEW_BNRELU ? W_BNRELU : W_PLAIN, W_PLAIN, dkernel, ws, ws_bytes, st,
+                     "unet_head_bwd(filter)");
+}
+size_t head_wgrad_workspace(int64_t M, int cin, int ncls) { return wgrad_workspace(M, cin, ncls); }
+}  // namespace unet

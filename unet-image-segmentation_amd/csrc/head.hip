@@ -1,0 +1,413 @@
+// Output layer + loss + metric kernels:
+//   head      : Conv2D(num_classes, 1, activation=sigmoid|softmax)   model/u_net.py:105-112
+//   dice/iou  : dice_coef / iou_coef / dice_loss / iou_loss            utils/metrics.py:6-62,
+//                                                                      utils/loss.py:9-48
+//   MeanIoU   : keras.metrics.MeanIoU(num_classes)                     scripts/train.py:231,
+//                                                                      scripts/benchmark.py:237-277
+// The head is HBM-bound (64 -> ncls per pixel): one lane per pixel, the (Cin x ncls)
+// kernel in LDS (broadcast reads).  Dice sums are per (image, class) over H*W: per-block
+// partials, then one fixed-order finalize in double.
+#include "view.h"
+
+namespace unet {
+
+int head_wgrad(const unet_view* x, int64_t M, const float* dlogit, int ncls, float* dkernel, void* ws,
+               size_t ws_bytes, hipStream_t st);
+size_t head_wgrad_workspace(int64_t M, int cin, int ncls);
+int colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, hipStream_t st);
+size_t colsum_workspace(int64_t rows, int cols);
+
+namespace {
+
+constexpr int kMaxCin = 256;
+constexpr int kMaxCls = 32;
+
+template <int MODE, int NC>
+__global__ __launch_bounds__(256) void head_fwd_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, float* __restrict__ prob) {
+    const int Cin = v.c0;
+    __shared__ float Ws[kMaxCin * NC];
+    __shared__ float bs[NC];
+    for (int i = threadIdx.x; i < Cin * NC; i += 256) {
+        const int k = i / NC, c = i % NC;
+        Ws[i] = c < ncls ? W[k * ncls + c] : 0.f;
+    }
+    if (threadIdx.x < NC) bs[threadIdx.x] = (threadIdx.x < ncls && bias) ? bias[threadIdx.x] : 0.f;
+    __syncthreads();
+    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+        float l[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) l[c] = bs[c];
+        for (int k = 0; k < Cin; k += 4) {
+            const float4 x = row_load4<MODE, false>(v, m, k);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                l[c] = fmaf(x.x, Ws[(k + 0) * NC + c], l[c]);
+                l[c] = fmaf(x.y, Ws[(k + 1) * NC + c], l[c]);
+                l[c] = fmaf(x.z, Ws[(k + 2) * NC + c], l[c]);
+                l[c] = fmaf(x.w, Ws[(k + 3) * NC + c], l[c]);
+            }
+        }
+        if (ncls == 1) {
+            prob[m] = 1.0f / (1.0f + expf(-l[0]));
+        } else {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (c < ncls) mx = fmaxf(mx, l[c]);
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                l[c] = c < ncls ? expf(l[c] - mx) : 0.f;
+                s += l[c];
+            }
+            const float inv = 1.0f / s;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (c < ncls) prob[m * ncls + c] = l[c] * inv;
+        }
+    }
+}
+
+// part[n][blk][3][ncls] = {sum t*p, sum t, sum p} over this block's pixels of image n
+template <int NC>
+__global__ __launch_bounds__(256) void dice_partial_kernel(const float* __restrict__ yt, const float* __restrict__ yp,
+                                                           int64_t hw, int ncls, int64_t ppb,
+                                                           float* __restrict__ part) {
+    const int n = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+    float I[NC], T[NC], P[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) I[c] = T[c] = P[c] = 0.f;
+    const int64_t p0 = (int64_t)blk * ppb;
+    const int64_t p1 = p0 + ppb < hw ? p0 + ppb : hw;
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+        const int64_t base = ((int64_t)n * hw + p) * ncls;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c < ncls) {
+                const float t = yt[base + c], q = yp[base + c];
+                I[c] = fmaf(t, q, I[c]);
+                T[c] += t;
+                P[c] += q;
+            }
+        }
+    }
+    __shared__ float red[4][3 * NC];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const float a = wave_sum(I[c]), b = wave_sum(T[c]), d = wave_sum(P[c]);
+        if (lane == 0) {
+            red[wave][c] = a;
+            red[wave][NC + c] = b;
+            red[wave][2 * NC + c] = d;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * NC) {
+        const int j = threadIdx.x / NC, c = threadIdx.x % NC;
+        if (c < ncls) {
+            const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+            part[(((int64_t)n * nblk + blk) * 3 + j) * ncls + c] = s;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void dice_finalize_kernel(const float* __restrict__ part, int N, int nblk, int ncls,
+                                                            float smooth, float* __restrict__ sums,
+                                                            float* __restrict__ result) {
+    double dsum = 0.0, isum = 0.0;
+    for (int idx = threadIdx.x; idx < N * ncls; idx += 256) {
+        const int n = idx / ncls, c = idx % ncls;
+        double I = 0.0, T = 0.0, P = 0.0;
+        for (int b = 0; b < nblk; ++b) {
+            const int64_t base = (((int64_t)n * nblk + b) * 3) * ncls + c;
+            I += part[base];
+            T += part[base + ncls];
+            P += part[base + 2 * ncls];
+        }
+        const float fi = (float)I, ft = (float)T, fp = (float)P;
+        if (sums) {
+            sums[idx * 3 + 0] = fi;
+            sums[idx * 3 + 1] = ft;
+            sums[idx * 3 + 2] = fp;
+        }
+        dsum += (double)((2.0f * fi + smooth) / (ft + fp + smooth));
+        isum += (double)((fi + smooth) / (ft + fp - fi + smooth));
+    }
+    __shared__ double rd[256], ri[256];
+    rd[threadIdx.x] = dsum;
+    ri[threadIdx.x] = isum;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            rd[threadIdx.x] += rd[threadIdx.x + s];
+            ri[threadIdx.x] += ri[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double cnt = (double)N * ncls;
+        const float dice = (float)(rd[0] / cnt);
+        result[0] = 1.0f - dice;
+        result[1] = dice;
+        result[2] = (float)(ri[0] / cnt);
+    }
+}
+
+// dlogit and dx for one pixel per lane
+template <int NC, int LOSS>
+__global__ __launch_bounds__(256) void head_bwd_kernel(int64_t M, int64_t hw, int Cin, int ncls,
+                                                       const float* __restrict__ W, const float* __restrict__ prob,
+                                                       const float* __restrict__ yt, const float* __restrict__ sums,
+                                                       float smooth, float gscale, float* __restrict__ dlogit,
+                                                       float* __restrict__ dx) {
+    __shared__ float Ws[kMaxCin * NC];
+    for (int i = threadIdx.x; i < Cin * NC; i += 256) {
+        const int k = i / NC, c = i % NC;
+        Ws[i] = c < ncls ? W[k * ncls + c] : 0.f;
+    }
+    __syncthreads();
+    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+        const int n = (int)(m / hw);
+        float p[NC], dl[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            p[c] = 0.f;
+            dl[c] = 0.f;
+            if (c < ncls) {
+                const float pc = prob[m * ncls + c], t = yt[m * ncls + c];
+                const float* s3 = sums + ((int64_t)n * ncls + c) * 3;
+                const float I = s3[0], T = s3[1], P = s3[2];
+                float dp;
+                if constexpr (LOSS == UNET_LOSS_DICE) {
+                    const float nm = 2.0f * I + smooth, den = T + P + smooth;
+                    dp = -gscale * (2.0f * t * den - nm) / (den * den);
+                } else {
+                    const float j = I + smooth, u = T + P - I + smooth;
+                    dp = -gscale * (t * u - j * (1.0f - t)) / (u * u);
+                }
+                p[c] = pc;
+                dl[c] = dp;
+            }
+        }
+        if (ncls == 1) {
+            dl[0] = dl[0] * p[0] * (1.0f - p[0]);
+        } else {
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) s = fmaf(dl[c], p[c], s);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) dl[c] = p[c] * (dl[c] - s);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            if (c < ncls) dlogit[m * ncls + c] = dl[c];
+        for (int k = 0; k < Cin; k += 4) {
+            float4 o = f4(0.f);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                o.x = fmaf(Ws[(k + 0) * NC + c], dl[c], o.x);
+                o.y = fmaf(Ws[(k + 1) * NC + c], dl[c], o.y);
+                o.z = fmaf(Ws[(k + 2) * NC + c], dl[c], o.z);
+                o.w = fmaf(Ws[(k + 3) * NC + c], dl[c], o.w);
+            }
+            st4(dx + m * Cin + k, o);
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void meaniou_small_kernel(const float* __restrict__ yt, const float* __restrict__ yp,
+                                                            int64_t count, float thr,
+                                                            unsigned long long* __restrict__ conf) {
+    unsigned int h[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) h[i] = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+        const long long t = (long long)yt[i];
+        const float q = yp[i];
+        const long long p = thr < 0.f ? (long long)q : (q > thr ? 1 : 0);
+        if (t >= 0 && t < K && p >= 0 && p < K) {
+#pragma unroll
+            for (int b = 0; b < K * K; ++b) h[b] += (t * K + p == b) ? 1u : 0u;
+        }
+    }
+    __shared__ unsigned int red[4][K * K];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < K * K; ++b) {
+        unsigned int v = h[b];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) red[wave][b] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < K * K) {
+        const unsigned int s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        if (s) atomicAdd(conf + threadIdx.x, (unsigned long long)s);
+    }
+}
+
+__global__ __launch_bounds__(256) void meaniou_kernel(const float* __restrict__ yt, const float* __restrict__ yp,
+                                                      int64_t count, int K, float thr,
+                                                      unsigned long long* __restrict__ conf) {
+    __shared__ unsigned int hist[kMaxCls * kMaxCls];
+    for (int b = threadIdx.x; b < K * K; b += 256) hist[b] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
+        const long long t = (long long)yt[i];
+        const float q = yp[i];
+        const long long p = thr < 0.f ? (long long)q : (q > thr ? 1 : 0);
+        if (t >= 0 && t < K && p >= 0 && p < K) atomicAdd(&hist[t * K + p], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < K * K; b += 256)
+        if (hist[b]) atomicAdd(conf + b, (unsigned long long)hist[b]);
+}
+
+int grid_for(int64_t work, int cap = 4096) {
+    int64_t g = cdiv(work, 256);
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+struct DicePlan {
+    int nblk;
+    int64_t ppb;
+};
+DicePlan dice_plan(int n, int64_t hw) {
+    DicePlan d;
+    int64_t want = cdiv(1024, n);
+    int64_t maxb = cdiv(hw, 1024);
+    int64_t b = want < maxb ? want : maxb;
+    if (b < 1) b = 1;
+    d.ppb = cdiv(hw, b);
+    d.nblk = (int)cdiv(hw, d.ppb);
+    return d;
+}
+
+}  // namespace
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" int unet_head_fwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
+                             const float* bias, float* prob, unet_stream_t stream) {
+    if (check_view(x, "unet_head_fwd", true)) return -1;
+    UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
+                   "unet_head_fwd: input view must be PLAIN or BNRELU");
+    UNET_CHECK_ARG(x->drop_rate == 0.f, "unet_head_fwd: dropout on the head input is not supported");
+    UNET_CHECK_ARG(x->c0 <= kMaxCin, "unet_head_fwd: Cin %d > %d", x->c0, kMaxCin);
+    UNET_CHECK_ARG(ncls >= 1 && ncls <= kMaxCls, "unet_head_fwd: num_classes %d out of [1,%d]", ncls, kMaxCls);
+    UNET_CHECK_ARG(kernel && prob && n > 0 && h > 0 && w > 0, "unet_head_fwd: bad args");
+    const DView v = make_dview(*x);
+    const int64_t M = (int64_t)n * h * w;
+    hipStream_t st = as_stream(stream);
+    const int grid = grid_for(M);
+    if (x->mode == UNET_VIEW_BNRELU) {
+        if (ncls == 1)
+            head_fwd_kernel<UNET_VIEW_BNRELU, 1><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+        else
+            head_fwd_kernel<UNET_VIEW_BNRELU, kMaxCls><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+    } else {
+        if (ncls == 1)
+            head_fwd_kernel<UNET_VIEW_PLAIN, 1><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+        else
+            head_fwd_kernel<UNET_VIEW_PLAIN, kMaxCls><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+    }
+    UNET_CHECK_LAUNCH("unet_head_fwd");
+    return 0;
+}
+
+extern "C" size_t unet_dice_workspace(int n, int64_t hw, int ncls) {
+    if (n <= 0 || hw <= 0 || ncls <= 0) return 0;
+    DicePlan d = dice_plan(n, hw);
+    return align_up((size_t)n * d.nblk * 3 * ncls * sizeof(float), 256);
+}
+
+extern "C" int unet_dice_fwd(const float* y_true, const float* y_pred, int n, int64_t hw, int ncls, float smooth,
+                             float* sums, float* result, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(y_true && y_pred && result && n > 0 && hw > 0, "unet_dice_fwd: bad args");
+    UNET_CHECK_ARG(ncls >= 1 && ncls <= kMaxCls, "unet_dice_fwd: num_classes %d out of [1,%d]", ncls, kMaxCls);
+    const size_t need = unet_dice_workspace(n, hw, ncls);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_dice_fwd: workspace %zu < %zu", ws_bytes, need);
+    DicePlan d = dice_plan(n, hw);
+    hipStream_t st = as_stream(stream);
+    float* part = static_cast<float*>(ws);
+    dim3 grid(d.nblk, n);
+    if (ncls == 1)
+        dice_partial_kernel<1><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    else
+        dice_partial_kernel<kMaxCls><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    UNET_CHECK_LAUNCH("unet_dice_fwd(partial)");
+    dice_finalize_kernel<<<1, 256, 0, st>>>(part, n, d.nblk, ncls, smooth, sums, result);
+    UNET_CHECK_LAUNCH("unet_dice_fwd(finalize)");
+    return 0;
+}
+
+extern "C" size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls) {
+    if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || ncls <= 0) return 0;
+    const int64_t M = (int64_t)n * h * w;
+    const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
+    size_t a = head_wgrad_workspace(M, cin, ncls);
+    size_t b = colsum_workspace(M, ncls);
+    return dl + (a > b ? a : b);
+}
+
+extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
+                             const float* prob, const float* y_true, const float* sums, float smooth, int loss_kind,
+                             float* dx, float* dkernel, float* dbias, void* ws, size_t ws_bytes,
+                             unet_stream_t stream) {
+    if (check_view(x, "unet_head_bwd", true)) return -1;
+    UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
+                   "unet_head_bwd: input view must be PLAIN or BNRELU");
+    UNET_CHECK_ARG(x->c0 <= kMaxCin, "unet_head_bwd: Cin %d > %d", x->c0, kMaxCin);
+    UNET_CHECK_ARG(ncls >= 1 && ncls <= kMaxCls, "unet_head_bwd: num_classes out of range");
+    UNET_CHECK_ARG(loss_kind == UNET_LOSS_DICE || loss_kind == UNET_LOSS_IOU, "unet_head_bwd: bad loss_kind");
+    UNET_CHECK_ARG(kernel && prob && y_true && sums && dx && dkernel && dbias, "unet_head_bwd: null pointer");
+    const size_t need = unet_head_bwd_workspace(n, h, w, x->c0, ncls);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_head_bwd: workspace %zu < %zu", ws_bytes, need);
+    const int64_t M = (int64_t)n * h * w;
+    const int64_t hw = (int64_t)h * w;
+    hipStream_t st = as_stream(stream);
+    float* dlogit = static_cast<float*>(ws);
+    const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
+    void* ws2 = static_cast<char*>(ws) + dl;
+    const size_t ws2_bytes = ws_bytes - dl;
+    const float gscale = 1.0f / (float)((int64_t)n * ncls);
+    const int grid = grid_for(M);
+#define UNET_HB(NC, L)                                                                                        \
+    head_bwd_kernel<NC, L><<<grid, 256, 0, st>>>(M, hw, x->c0, ncls, kernel, prob, y_true, sums, smooth, gscale, \
+                                                 dlogit, dx)
+    if (ncls == 1) {
+        if (loss_kind == UNET_LOSS_DICE) UNET_HB(1, UNET_LOSS_DICE);
+        else UNET_HB(1, UNET_LOSS_IOU);
+    } else {
+        if (loss_kind == UNET_LOSS_DICE) UNET_HB(kMaxCls, UNET_LOSS_DICE);
+        else UNET_HB(kMaxCls, UNET_LOSS_IOU);
+    }
+#undef UNET_HB
+    UNET_CHECK_LAUNCH("unet_head_bwd");
+    int rc = head_wgrad(x, M, dlogit, ncls, dkernel, ws2, ws2_bytes, st);
+    if (rc) return rc;
+    return colsum(dlogit, M, ncls, dbias, ws2, ws2_bytes, st);
+}
+
+extern "C" int unet_meaniou_update(const float* y_true, const float* y_pred, int64_t count, int num_classes,
+                                   float threshold, uint64_t* confusion, unet_stream_t stream) {
+    UNET_CHECK_ARG(y_true && y_pred && confusion && count >= 0, "unet_meaniou_update: bad args");
+    UNET_CHECK_ARG(num_classes >= 1 && num_classes <= kMaxCls, "unet_meaniou_update: num_classes out of [1,%d]",
+                   kMaxCls);
+    if (count == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    const int grid = grid_for(count, 2048);
+    auto* conf = reinterpret_cast<unsigned long long*>(confusion);
+    if (num_classes == 2)
+        meaniou_small_kernel<2><<<grid, 256, 0, st>>>(y_true, y_pred, count, threshold, conf);
+    else
+        meaniou_kernel<<<grid, 256, 0, st>>>(y_true, y_pred, count, num_classes, threshold, conf);
+    UNET_CHECK_LAUNCH("unet_meaniou_update");
+    return 0;
+}

@@ -1,0 +1,360 @@
+"""The U-Net train / predict step on MI355X: a fixed schedule of libunet_hip.so kernels.
+
+Replaces what Keras + TensorFlow do for the reference's hot path:
+  forward   model/u_net.py:28-116 (U_NET), conv_block :5-26
+  loss      utils/loss.py:9-48, utils/metrics.py:6-62
+  backward  the GradientTape of `model.fit` (scripts/train.py:308)
+  update    keras.optimizers.AdamW (scripts/train.py:226) -> optim.AdamW
+
+Data layout in HBM (per GPU, batch N):
+  * conv_block outputs are stored RAW (pre-BatchNorm z, NHWC); the BN affine + ReLU, the
+    2x2 max-pool, the skip concat and dropout are applied by the consumer on load
+    (activation views), so activations a = relu(bn(z)), pooled tensors and concat buffers
+    are never materialised;
+  * each block also keeps its depthwise output y (the pointwise weight gradient needs it);
+  * trainable variables / gradients / Adam moments: one flat buffer each (params.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import ops
+from .ops import View
+from .params import FILTERS, VarSpec, check_input_size, count_params, flat_layout, init_weights, unet_variables
+
+BN_EPS = 1e-3       # keras BatchNormalization default epsilon
+BN_MOMENTUM = 0.99  # keras BatchNormalization default momentum
+SMOOTH = 1e-7       # K.epsilon() (utils/metrics.py:4)
+DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
+
+
+def _mix64(*vals: int) -> int:
+    z = 0x243F6A8885A308D3
+    for v in vals:
+        z = (z ^ (int(v) & 0xFFFFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF
+        z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        z ^= z >> 31
+    return z
+
+
+@dataclass
+class Block:
+    """One conv_block (SeparableConv2D -> BatchNormalization -> ReLU)."""
+
+    name: str
+    cin: int
+    cout: int
+    level: int  # spatial size = input / 2**level
+
+
+@dataclass
+class BlockBufs:
+    y: torch.Tensor
+    z: torch.Tensor
+    part: torch.Tensor
+    mean: torch.Tensor
+    rstd: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+    da: torch.Tensor  # gradient w.r.t. this block's output activation
+
+
+@dataclass
+class Acts:
+    n: int
+    blocks: Dict[str, BlockBufs]
+    up: Dict[str, torch.Tensor]
+    dup: Dict[str, torch.Tensor]
+    prob: torch.Tensor
+    dz: torch.Tensor
+    dy: torch.Tensor
+    sums: torch.Tensor
+    result: torch.Tensor
+
+
+class UNetEngine:
+    """Device-resident U-Net with explicit forward / backward schedules."""
+
+    def __init__(self, input_size: Sequence[int], num_classes: int = 1, dropout_rate: float = 0.2,
+                 use_batch_norm: bool = True, filters: Sequence[int] = FILTERS, device=None, seed: int = 2301):
+        self.h, self.w, self.c = check_input_size(input_size, len(filters))
+        if num_classes < 1:
+            raise ValueError("num_classes must be >= 1")
+        if not 0.0 <= dropout_rate < 1.0:
+            raise ValueError("dropout_rate must be in [0, 1)")
+        if not torch.cuda.is_available():
+            raise RuntimeError("UNetEngine needs a HIP device (MI355X); there is no CPU execution path")
+        L.load()
+        self.num_classes = int(num_classes)
+        self.dropout_rate = float(dropout_rate)
+        self.use_bn = bool(use_batch_norm)
+        self.filters = tuple(int(f) for f in filters)
+        self.device = torch.device(device if device is not None else "cuda")
+        self.seed = int(seed)
+        self.specs: List[VarSpec] = unet_variables(self.c, self.num_classes, self.use_bn, self.filters)
+        self.spec_by_name = {s.name: s for s in self.specs}
+        self.train_layout = flat_layout(self.specs, True)
+        self.stat_layout = flat_layout(self.specs, False)
+        self.params = torch.zeros(self.train_layout.total, dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros_like(self.params)
+        self.stats = torch.zeros(self.stat_layout.total, dtype=torch.float32, device=self.device)
+        self.vars: Dict[str, torch.Tensor] = {}
+        self.gvars: Dict[str, torch.Tensor] = {}
+        for s in self.specs:
+            if s.trainable:
+                o = self.train_layout.offsets[s.name]
+                self.vars[s.name] = self.params[o:o + s.size].view(s.shape)
+                self.gvars[s.name] = self.grads[o:o + s.size].view(s.shape)
+            else:
+                o = self.stat_layout.offsets[s.name]
+                self.vars[s.name] = self.stats[o:o + s.size].view(s.shape)
+        self.set_weights_dict(init_weights(self.specs, self.seed))
+        self._build_plan()
+        self._acts: Dict[int, Acts] = {}
+        self.step_count = 0
+        self.grad_hook: Optional[Callable[[int], None]] = None  # called with a flat-offset low-water mark
+
+    # ------------------------------------------------------------------ weights ------
+    def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
+        for name, arr in weights.items():
+            if name not in self.vars:
+                raise KeyError(f"unknown variable {name}")
+            t = self.vars[name]
+            a = np.asarray(arr, dtype=np.float32)
+            if tuple(a.shape) != tuple(t.shape):
+                raise ValueError(f"{name}: shape {a.shape} != {tuple(t.shape)}")
+            t.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(self.device))
+
+    def get_weights_dict(self) -> Dict[str, np.ndarray]:
+        return {s.name: self.vars[s.name].detach().cpu().numpy().copy() for s in self.specs}
+
+    def count_params(self):
+        return count_params(self.specs)
+
+    # --------------------------------------------------------------------- plan ------
+    def _build_plan(self):
+        f = self.filters
+        self.enc: List[tuple] = []
+        c = self.c
+        for i, fi in enumerate(f):
+            b1 = Block(f"enc{i + 1}_block1", c, fi, i)
+            b2 = Block(f"enc{i + 1}_block2", fi, fi, i)
+            self.enc.append((f"enc{i + 1}", b1, b2))
+            c = fi
+        d = len(f)
+        bn = 2 * f[-1]
+        self.bneck = (Block("bneck_block1", c, bn, d), Block("bneck_block2", bn, bn, d))
+        self.dec: List[tuple] = []
+        c = bn
+        for i, fi in enumerate(reversed(f)):
+            stage = len(f) - i
+            lvl = stage - 1
+            self.dec.append((f"dec{stage}", fi, c, Block(f"dec{stage}_block1", 2 * fi, fi, lvl),
+                             Block(f"dec{stage}_block2", fi, fi, lvl)))
+            c = fi
+        self.blocks: List[Block] = [b for _, b1, b2 in self.enc for b in (b1, b2)] + list(self.bneck) + \
+                                   [b for *_, b1, b2 in self.dec for b in (b1, b2)]
+
+    def _dims(self, level: int):
+        return self.h >> level, self.w >> level
+
+    def acts(self, n: int) -> Acts:
+        a = self._acts.get(n)
+        if a is not None:
+            return a
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        blocks = {}
+        max_in = max_out = 0
+        for b in self.blocks:
+            h, w = self._dims(b.level)
+            m = n * h * w
+            max_in = max(max_in, m * b.cin)
+            max_out = max(max_out, m * b.cout)
+            blocks[b.name] = BlockBufs(
+                y=torch.empty((n, h, w, b.cin), **f32), z=torch.empty((n, h, w, b.cout), **f32),
+                part=torch.empty(ops.bn_partials_numel(m, b.cout), **f32),
+                mean=torch.zeros(b.cout, **f32), rstd=torch.zeros(b.cout, **f32),
+                scale=torch.zeros(b.cout, **f32), shift=torch.zeros(b.cout, **f32),
+                da=torch.empty((n, h, w, b.cout), **f32))
+        up, dup = {}, {}
+        for stage, fi, cin, b1, b2 in self.dec:
+            h, w = self._dims(b1.level)
+            up[stage] = torch.empty((n, h, w, fi), **f32)
+            dup[stage] = torch.empty((n, h, w, fi), **f32)
+        a = Acts(n=n, blocks=blocks, up=up, dup=dup,
+                 prob=torch.empty((n, self.h, self.w, self.num_classes), **f32),
+                 dz=torch.empty(max_out, **f32), dy=torch.empty(max_in, **f32),
+                 sums=torch.zeros(n * self.num_classes * 3, **f32), result=torch.zeros(3, **f32))
+        self._acts[n] = a
+        return a
+
+    def release_buffers(self):
+        self._acts.clear()
+
+    # ------------------------------------------------------------------ forward ------
+    def _bn(self, name):
+        if self.use_bn:
+            return (self.vars[f"{name}_bn/gamma"], self.vars[f"{name}_bn/beta"], self.vars[f"{name}_bn/moving_mean"],
+                    self.vars[f"{name}_bn/moving_variance"])
+        return None, self.vars[f"{name}_sepconv/bias"], None, None
+
+    def _block_fwd(self, A: Acts, b: Block, view: View, training: bool) -> View:
+        n = A.n
+        h, w = self._dims(b.level)
+        m = n * h * w
+        bb = A.blocks[b.name]
+        ops.dwconv3x3_fwd(view, n, h, w, self.vars[f"{b.name}_sepconv/depthwise_kernel"], bb.y)
+        gamma, beta, mm, mv = self._bn(b.name)
+        if training and self.use_bn:
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, self.vars[f"{b.name}_sepconv/pointwise_kernel"], bb.z, bb.part)
+            ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
+                            bb.scale, bb.shift)
+        else:
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, self.vars[f"{b.name}_sepconv/pointwise_kernel"], bb.z, None)
+            ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
+        return View.bnrelu(bb.z, bb.scale, bb.shift)
+
+    def drop_seeds(self, step: int) -> Dict[str, int]:
+        return {s: _mix64(self.seed, step, i + 1) for i, s in enumerate(DROP_SITES)}
+
+    def forward(self, x: torch.Tensor, training: bool = False, seeds: Optional[Dict[str, int]] = None) -> torch.Tensor:
+        """Forward pass (model/u_net.py:55-112).  x: (N, H, W, C) float32 NHWC on the device.
+        training=True uses batch statistics (and updates the moving ones) and dropout."""
+        if x.dim() != 4 or tuple(x.shape[1:]) != (self.h, self.w, self.c):
+            raise ValueError(f"expected input (N, {self.h}, {self.w}, {self.c}), got {tuple(x.shape)}")
+        x = x.contiguous()
+        n = x.shape[0]
+        A = self.acts(n)
+        drop = training and self.dropout_rate > 0.0
+        if drop and seeds is None:
+            seeds = self.drop_seeds(self.step_count + 1)
+        v = View.plain(x)
+        for stage, b1, b2 in self.enc:
+            v = self._block_fwd(A, b1, v, training)
+            self._block_fwd(A, b2, v, training)
+            bb = A.blocks[b2.name]
+            v = View.pool_bnrelu(bb.z, bb.scale, bb.shift)
+        v = self._block_fwd(A, self.bneck[0], v, training)
+        v = self._block_fwd(A, self.bneck[1], v, training)
+        if drop:
+            v = v.dropout(self.dropout_rate, seeds["bneck_dropout"])
+        for i, (stage, fi, cin, b1, b2) in enumerate(self.dec):
+            h, w = self._dims(b1.level + 1)
+            ops.conv_transpose2x2_fwd(v, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
+                                      self.vars[f"{stage}_upsample/bias"], A.up[stage])
+            skip = A.blocks[self.enc[len(self.enc) - 1 - i][2].name]
+            v = View.concat(A.up[stage], skip.z, skip.scale, skip.shift)
+            if drop and i < len(self.dec) - 1:
+                v = v.dropout(self.dropout_rate, seeds[f"{stage}_dropout"])
+            v = self._block_fwd(A, b1, v, training)
+            v = self._block_fwd(A, b2, v, training)
+        ops.head_fwd(v, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
+                     self.vars["output_mask/bias"], A.prob)
+        self._last_seeds = seeds
+        return A.prob
+
+    def loss(self, y_true: torch.Tensor, n: int) -> torch.Tensor:
+        """dice_loss / dice_coef / iou_coef of the last forward -> result[0:3] (device)."""
+        A = self.acts(n)
+        ops.dice_fwd(y_true, A.prob, n, self.h * self.w, self.num_classes, SMOOTH, A.sums, A.result)
+        return A.result
+
+    # ----------------------------------------------------------------- backward ------
+    def _grads_ready(self, name: str):
+        if self.grad_hook is not None:
+            self.grad_hook(self.train_layout.offsets[name])
+
+    def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0):
+        n = A.n
+        h, w = self._dims(b.level)
+        m = n * h * w
+        bb = A.blocks[b.name]
+        dz = A.dz[:m * b.cout]
+        dy = A.dy[:m * b.cin]
+        if self.use_bn:
+            dgamma, dbeta = self.gvars[f"{b.name}_bn/gamma"], self.gvars[f"{b.name}_bn/beta"]
+        else:
+            dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
+        ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
+                        drop_seed, dgamma, dbeta, dz)
+        pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
+        dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
+        ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, self.gvars[f"{b.name}_sepconv/pointwise_kernel"])
+        ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
+        ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, self.gvars[f"{b.name}_sepconv/depthwise_kernel"])
+        if dx0 is not None:
+            ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
+        self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
+
+    def _view_of(self, A: Acts, b: Block) -> View:
+        bb = A.blocks[b.name]
+        return View.bnrelu(bb.z, bb.scale, bb.shift)
+
+    def backward(self, y_true: torch.Tensor, loss_kind: int = L.LOSS_DICE) -> None:
+        """Gradients of the loss of the last training forward into self.grads."""
+        A = self._acts_last
+        n = A.n
+        seeds = self._last_seeds
+        drop = seeds is not None and self.dropout_rate > 0.0
+        last = self.dec[-1][4]
+        ops.head_bwd(self._view_of(A, last), n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
+                     A.prob, y_true, A.sums, SMOOTH, loss_kind, A.blocks[last.name].da,
+                     self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"])
+        self._grads_ready("output_mask/kernel")
+        nd = len(self.dec)
+        for i in reversed(range(nd)):
+            stage, fi, cin, b1, b2 = self.dec[i]
+            self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da)
+            enc_b2 = self.enc[len(self.enc) - 1 - i][2]
+            sk = A.blocks[enc_b2.name]
+            vin = View.concat(A.up[stage], sk.z, sk.scale, sk.shift)
+            if drop and i < nd - 1:
+                vin = vin.dropout(self.dropout_rate, seeds[f"{stage}_dropout"])
+            # skip half of the gradient is STORED into the encoder block's da (first contribution)
+            self._block_bwd(A, b1, vin, A.dup[stage], sk.da)
+            prev = self.dec[i - 1][4] if i > 0 else self.bneck[1]
+            xv = self._view_of(A, prev)
+            if i == 0 and drop:
+                xv = xv.dropout(self.dropout_rate, seeds["bneck_dropout"])
+            h, w = self._dims(b1.level + 1)
+            ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
+                                      A.blocks[prev.name].da, self.gvars[f"{stage}_upsample/kernel"],
+                                      self.gvars[f"{stage}_upsample/bias"])
+            self._grads_ready(f"{stage}_upsample/kernel")
+        b1, b2 = self.bneck
+        self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da,
+                        drop_rate=self.dropout_rate if drop else 0.0,
+                        drop_seed=seeds["bneck_dropout"] if drop else 0)
+        e4 = A.blocks[self.enc[-1][2].name]
+        # pooled half ACCUMULATES into the encoder block's da (the skip half is already there)
+        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da)
+        for j in reversed(range(len(self.enc))):
+            stage, e1, e2 = self.enc[j]
+            self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da)
+            if j > 0:
+                pb = A.blocks[self.enc[j - 1][2].name]
+                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da)
+            else:
+                self._block_bwd(A, e1, View.plain(self._x_last), None)
+
+    # --------------------------------------------------------------- train step ------
+    def forward_train(self, x: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:
+        self.step_count += 1
+        seeds = self.drop_seeds(self.step_count) if self.dropout_rate > 0 else None
+        x = x.contiguous()
+        self.forward(x, training=True, seeds=seeds)
+        self._x_last = x
+        self._acts_last = self.acts(x.shape[0])
+        return self.loss(y_true.contiguous(), x.shape[0])
+
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """Inference forward (BN moving stats, no dropout); returns a new (N, H, W, ncls) tensor."""
+        return self.forward(x, training=False).clone()

@@ -1,0 +1,234 @@
+"""Keras-Model-like facade over UNetEngine: what `U_NET(...)` returns.
+
+Mirrors the parts of tf.keras.Model the reference uses: compile (scripts/train.py:227-234),
+fit (:308-316), predict (scripts/inference.py:116, benchmark.py:254), summary (:235),
+weights by Keras names, save / load of the trained weights.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .dp import GradBucketer
+from .engine import UNetEngine
+from .metrics import MeanIoU, as_device_tensor
+from .optim import AdamW
+from .params import FILTERS
+
+
+def _loss_kind(loss) -> int:
+    name = loss if isinstance(loss, str) else getattr(loss, "__name__", "")
+    if name in ("dice_loss", "dice"):
+        return L.LOSS_DICE
+    if name in ("iou_loss", "jaccard_loss", "iou"):
+        return L.LOSS_IOU
+    raise ValueError(f"unsupported loss {loss!r}: the engine implements dice_loss and iou_loss/jaccard_loss")
+
+
+class History:
+    def __init__(self):
+        self.history: Dict[str, List[float]] = {}
+        self.epoch: List[int] = []
+
+
+class UNetModel:
+    def __init__(self, input_size, num_classes: int = 1, dropout_rate: float = 0.2, use_batch_norm: bool = True,
+                 filters: Sequence[int] = FILTERS, device=None, seed: int = 2301, name: str = "U-NET-Segmentation"):
+        self.engine = UNetEngine(input_size, num_classes, dropout_rate, use_batch_norm, filters, device, seed)
+        self.name = name
+        self.input_shape = (None, self.engine.h, self.engine.w, self.engine.c)
+        self.output_shape = (None, self.engine.h, self.engine.w, num_classes)
+        self.optimizer: Optional[AdamW] = None
+        self.loss_kind = L.LOSS_DICE
+        self.metric_names: List[str] = []
+        self.mean_iou: Optional[MeanIoU] = None
+        self.bucketer: Optional[GradBucketer] = None
+        self.stop_training = False
+
+    # --------------------------------------------------------------------- keras API ---
+    @property
+    def num_classes(self):
+        return self.engine.num_classes
+
+    def compile(self, optimizer=None, loss="dice_loss", metrics: Optional[Iterable] = None):
+        self.optimizer = optimizer if optimizer is not None else AdamW()
+        self.loss_kind = _loss_kind(loss)
+        self.metric_names = []
+        self.mean_iou = None
+        for m in metrics or []:
+            if isinstance(m, MeanIoU):
+                self.mean_iou = m
+                self.metric_names.append(m.name)
+            else:
+                nm = m if isinstance(m, str) else getattr(m, "__name__", str(m))
+                if nm not in ("dice_coef", "iou_coef"):
+                    raise ValueError(f"unsupported metric {m!r}")
+                self.metric_names.append(nm)
+
+    def enable_data_parallel(self, bucket_bytes: int = 6 << 20, group=None):
+        """Average gradients over torch.distributed ranks each step (bucketed, overlapped)."""
+        self.bucketer = GradBucketer(self.engine.grads, bucket_bytes, group)
+        self.engine.grad_hook = self.bucketer.ready
+
+    def train_step(self, x, y) -> torch.Tensor:
+        """One optimisation step; returns the device vector [loss, dice_coef, iou_coef]
+        (asynchronous: nothing here waits for the GPU)."""
+        if self.optimizer is None:
+            self.compile()
+        x = as_device_tensor(x, self.engine.device)
+        y = as_device_tensor(y, self.engine.device)
+        res = self.engine.forward_train(x, y)
+        if self.mean_iou is not None:
+            self.mean_iou.update_state(y, self.engine.acts(x.shape[0]).prob)
+        if self.loss_kind == L.LOSS_IOU:
+            res = res.clone()
+            res[0] = 1.0 - res[2]
+        self.engine.backward(y, self.loss_kind)
+        scale = self.bucketer.finish() if self.bucketer is not None else 1.0
+        self.optimizer.apply(self.engine.params, self.engine.grads, scale)
+        return res
+
+    def test_step(self, x, y) -> torch.Tensor:
+        x = as_device_tensor(x, self.engine.device)
+        y = as_device_tensor(y, self.engine.device)
+        self.engine.forward(x, training=False)
+        res = self.engine.loss(y, x.shape[0])
+        if self.mean_iou is not None:
+            self.mean_iou.update_state(y, self.engine.acts(x.shape[0]).prob)
+        if self.loss_kind == L.LOSS_IOU:
+            res = res.clone()
+            res[0] = 1.0 - res[2]
+        return res
+
+    def __call__(self, x, training: bool = False) -> torch.Tensor:
+        x = as_device_tensor(x, self.engine.device)
+        return self.engine.forward(x, training=training).clone()
+
+    def predict(self, x, batch_size: Optional[int] = None, verbose: int = 0):
+        """model.predict: numpy in -> numpy out, tensor in -> device tensor out."""
+        is_np = not isinstance(x, torch.Tensor)
+        xt = as_device_tensor(x, self.engine.device)
+        n = xt.shape[0]
+        bs = batch_size or 32
+        outs = [self.engine.predict(xt[i:i + bs]) for i in range(0, n, bs)]
+        out = torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+        return out.cpu().numpy() if is_np else out
+
+    def _log_values(self, res: torch.Tensor, prefix: str = "") -> Dict[str, float]:
+        r = res.detach().cpu().numpy()
+        out = {f"{prefix}loss": float(r[0])}
+        for nm in self.metric_names:
+            if nm == "dice_coef":
+                out[prefix + nm] = float(r[1])
+            elif nm == "iou_coef":
+                out[prefix + nm] = float(r[2])
+        return out
+
+    def fit(self, x=None, epochs: int = 1, steps_per_epoch: Optional[int] = None, validation_data=None,
+            validation_steps: Optional[int] = None, callbacks=None, verbose: int = 1) -> History:
+        """Keras fit over a generator of (image_batch, mask_batch) (scripts/train.py:308-316).
+        Per-epoch logs: loss and metrics as batch means (Keras MeanMetricWrapper) and MeanIoU
+        over the epoch's confusion matrix; val_* from validation_data."""
+        from .callbacks import CallbackList
+        if self.optimizer is None:
+            self.compile()
+        cbs = CallbackList(callbacks or [], self)
+        hist = History()
+        self.stop_training = False
+        it = iter(x)
+        cbs.on_train_begin()
+        for epoch in range(epochs):
+            cbs.on_epoch_begin(epoch)
+            if self.mean_iou is not None:
+                self.mean_iou.reset_state()
+            acc = None
+            nsteps = 0
+            t0 = time.time()
+            for step in range(steps_per_epoch or 1):
+                xb, yb = next(it)
+                res = self.train_step(xb, yb)
+                acc = res.detach().clone() if acc is None else acc + res
+                nsteps += 1
+            logs = self._log_values(acc / nsteps)
+            if self.mean_iou is not None:
+                self.mean_iou.all_reduce()
+                logs[self.mean_iou.name] = self.mean_iou.result()
+            if validation_data is not None:
+                logs.update(self.evaluate(validation_data, steps=validation_steps, prefix="val_"))
+            for k, v in logs.items():
+                hist.history.setdefault(k, []).append(v)
+            hist.epoch.append(epoch)
+            if verbose:
+                dt = time.time() - t0
+                body = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items())
+                print(f"Epoch {epoch + 1}/{epochs} - {nsteps} steps - {dt:.1f}s - {body}", flush=True)
+            cbs.on_epoch_end(epoch, logs)
+            if self.stop_training:
+                break
+        cbs.on_train_end()
+        return hist
+
+    def evaluate(self, data, steps: Optional[int] = None, prefix: str = "") -> Dict[str, float]:
+        it = iter(data)
+        if self.mean_iou is not None:
+            saved = self.mean_iou.confusion.clone()
+            self.mean_iou.reset_state()
+        acc, n = None, 0
+        for _ in range(steps or 1):
+            xb, yb = next(it)
+            res = self.test_step(xb, yb)
+            acc = res.detach().clone() if acc is None else acc + res
+            n += 1
+        logs = self._log_values(acc / n, prefix)
+        if self.mean_iou is not None:
+            self.mean_iou.all_reduce()
+            logs[prefix + self.mean_iou.name] = self.mean_iou.result()
+            self.mean_iou.confusion.copy_(saved)
+        return logs
+
+    # ------------------------------------------------------------------- weights -------
+    @property
+    def weights(self) -> List[str]:
+        return [s.name for s in self.engine.specs]
+
+    def get_weights(self) -> List[np.ndarray]:
+        w = self.engine.get_weights_dict()
+        return [w[s.name] for s in self.engine.specs]
+
+    def set_weights(self, weights: List[np.ndarray]):
+        if len(weights) != len(self.engine.specs):
+            raise ValueError(f"expected {len(self.engine.specs)} arrays, got {len(weights)}")
+        self.engine.set_weights_dict({s.name: w for s, w in zip(self.engine.specs, weights)})
+
+    def save_weights(self, path: str):
+        """Neutral weight file: .npz keyed by Keras weight names, Keras layouts."""
+        w = self.engine.get_weights_dict()
+        np.savez(path, **{k.replace("/", ":"): v for k, v in w.items()})
+
+    save = save_weights
+
+    def load_weights(self, path: str):
+        with np.load(path, allow_pickle=False) as z:
+            self.engine.set_weights_dict({k.replace(":", "/"): z[k] for k in z.files})
+
+    def count_params(self) -> int:
+        return sum(self.engine.count_params())
+
+    def summary(self, line_length: int = 100, print_fn=print):
+        tr, nt = self.engine.count_params()
+        print_fn(f'Model: "{self.name}"')
+        print_fn("_" * line_length)
+        print_fn(f"{'Variable':60s}{'Shape':>25s}{'Trainable':>15s}")
+        print_fn("=" * line_length)
+        for s in self.engine.specs:
+            print_fn(f"{s.name:60s}{str(s.shape):>25s}{str(s.trainable):>15s}")
+        print_fn("=" * line_length)
+        print_fn(f"Total params: {tr + nt:,}")
+        print_fn(f"Trainable params: {tr:,}")
+        print_fn(f"Non-trainable params: {nt:,}")
+        print_fn("_" * line_length)

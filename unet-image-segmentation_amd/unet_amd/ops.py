@@ -1,0 +1,332 @@
+"""Torch-tensor front end of the C-ABI: argument checking, pointers, streams, workspaces.
+
+PyTorch is plumbing here (device memory, the current HIP stream, torch.distributed);
+every computation is a libunet_hip.so kernel.  Tensors must be contiguous float32 on a
+HIP device; ops run asynchronously on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, replace
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import UnetView
+
+Tensor = torch.Tensor
+
+
+def _ptr(t: Optional[Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(t: Tensor, name: str, numel: Optional[int] = None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device (HIP) tensor; there is no CPU path")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name}: expected {numel} elements, got {t.numel()}")
+
+
+class _Workspace:
+    """Per-(device, stream) growable scratch buffer (stream order makes reuse safe)."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, nbytes: int, device) -> Tensor:
+        key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            nb = max(int(nbytes * 1.25), 1 << 20)
+            buf = torch.empty(nb, dtype=torch.uint8, device=device)
+            self._bufs[key] = buf
+        return buf
+
+
+WORKSPACE = _Workspace()
+
+
+class KernelTimer:
+    """Brackets selected C-ABI ops with HIP events on the stream they are launched on
+    (torch's current stream) and accumulates their algorithmic flops / bytes, so a bench
+    can report achieved throughput of one kernel over a timed region."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.records = []  # (name, flops, bytes, start_event, end_event)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, fl, nb, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += fl
+            d["bytes"] += nb
+        return out
+
+
+TIMER: Optional[KernelTimer] = None
+
+
+def _call(name: str, work, *args):
+    """L.call, bracketed by HIP events when TIMER selects `name`; work = (flops, bytes)."""
+    t = TIMER
+    if t is None or name not in t.names:
+        L.call(name, *args)
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    L.call(name, *args)
+    e1.record()
+    t.records.append((name, float(work[0]), float(work[1]), e0, e1))
+
+
+def _ws(nbytes: int, device):
+    if nbytes <= 0:
+        return None, 0
+    buf = WORKSPACE.get(nbytes, device)
+    return _ptr(buf), buf.numel()
+
+
+# ---------------------------------------------------------------------------- views ---
+@dataclass
+class View:
+    """Python side of `unet_view`: how a layer reads its logical input (see unet_hip.h)."""
+
+    mode: int
+    src0: Tensor
+    c0: int
+    scale0: Optional[Tensor] = None
+    shift0: Optional[Tensor] = None
+    src1: Optional[Tensor] = None
+    c1: int = 0
+    scale1: Optional[Tensor] = None
+    shift1: Optional[Tensor] = None
+    drop_rate: float = 0.0
+    drop_seed: int = 0
+
+    @property
+    def channels(self) -> int:
+        return self.c0 + (self.c1 if self.mode == L.VIEW_CONCAT else 0)
+
+    @staticmethod
+    def plain(x: Tensor) -> "View":
+        return View(L.VIEW_PLAIN, x, x.shape[-1])
+
+    @staticmethod
+    def bnrelu(z: Tensor, scale: Tensor, shift: Tensor) -> "View":
+        return View(L.VIEW_BNRELU, z, z.shape[-1], scale, shift)
+
+    @staticmethod
+    def pool_bnrelu(z: Tensor, scale: Tensor, shift: Tensor) -> "View":
+        return View(L.VIEW_POOL_BNRELU, z, z.shape[-1], scale, shift)
+
+    @staticmethod
+    def concat(up: Tensor, skip_z: Tensor, scale: Tensor, shift: Tensor) -> "View":
+        return View(L.VIEW_CONCAT, up, up.shape[-1], None, None, skip_z, skip_z.shape[-1], scale, shift)
+
+    def dropout(self, rate: float, seed: int) -> "View":
+        return replace(self, drop_rate=float(rate), drop_seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+    def c_struct(self) -> UnetView:
+        for name in ("src0", "scale0", "shift0", "src1", "scale1", "shift1"):
+            t = getattr(self, name)
+            if t is not None:
+                _check(t, f"view.{name}")
+        v = UnetView()
+        v.mode = self.mode
+        v.c0 = self.c0
+        v.c1 = self.c1 if self.mode == L.VIEW_CONCAT else 0
+        v.src0 = self.src0.data_ptr()
+        v.scale0 = self.scale0.data_ptr() if self.scale0 is not None else None
+        v.shift0 = self.shift0.data_ptr() if self.shift0 is not None else None
+        v.src1 = self.src1.data_ptr() if self.src1 is not None else None
+        v.scale1 = self.scale1.data_ptr() if self.scale1 is not None else None
+        v.shift1 = self.shift1.data_ptr() if self.shift1 is not None else None
+        v.drop_rate = self.drop_rate
+        v.drop_seed = self.drop_seed
+        return v
+
+
+def view_materialize(x: View, n: int, h: int, w: int, out: Tensor) -> Tensor:
+    _check(out, "out", n * h * w * x.channels)
+    vs = x.c_struct()
+    L.call("unet_view_materialize", ctypes.byref(vs), n, h, w, _ptr(out), _stream())
+    return out
+
+
+# --------------------------------------------------------------- SeparableConv2D ---
+def dwconv3x3_fwd(x: View, n: int, h: int, w: int, dk: Tensor, out: Tensor) -> Tensor:
+    C = x.channels
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(out, "out", n * h * w * C)
+    vs = x.c_struct()
+    _call("unet_dwconv3x3_fwd", (18.0 * n * h * w * C, 4.0 * (2 * n * h * w * C + 9 * C)), ctypes.byref(vs), n, h,
+          w, _ptr(dk), _ptr(out), _stream())
+    return out
+
+
+def dwconv3x3_bwd_data(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Tensor, dx1: Optional[Tensor] = None):
+    C = x.channels
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(dy, "dy", n * h * w * C)
+    _check(dx0, "dx0")
+    if dx1 is not None:
+        _check(dx1, "dx1")
+    vs = x.c_struct()
+    L.call("unet_dwconv3x3_bwd_data", ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dx0), _ptr(dx1),
+           _stream())
+
+
+def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
+    C = x.channels
+    _check(dy, "dy", n * h * w * C)
+    _check(ddk, "d_depthwise_kernel", 9 * C)
+    ws, wsb = _ws(L.query("unet_dwconv3x3_bwd_filter_workspace", n, h, w, C), dy.device)
+    vs = x.c_struct()
+    L.call("unet_dwconv3x3_bwd_filter", ctypes.byref(vs), n, h, w, _ptr(dy), _ptr(ddk), ws, wsb, _stream())
+
+
+def bn_partials_numel(m: int, c: int) -> int:
+    return L.query("unet_bn_partials_size", m, c) // 4
+
+
+def pointwise_fwd(y: Tensor, m: int, cin: int, cout: int, pk: Tensor, z: Tensor, partials: Optional[Tensor] = None):
+    _check(y, "y", m * cin)
+    _check(pk, "pointwise_kernel", cin * cout)
+    _check(z, "z", m * cout)
+    if partials is not None:
+        _check(partials, "bn_partials", bn_partials_numel(m, cout))
+    _call("unet_pointwise_fwd", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(y), m, cin,
+          cout, _ptr(pk), _ptr(z), _ptr(partials), _stream())
+
+
+def pointwise_bwd_data(dz: Tensor, m, cin, cout, pk: Tensor, dy: Tensor):
+    _check(dz, "dz", m * cout)
+    _check(pk, "pointwise_kernel", cin * cout)
+    _check(dy, "dy", m * cin)
+    _call("unet_pointwise_bwd_data", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(dz), m,
+          cin, cout, _ptr(pk), _ptr(dy), _stream())
+
+
+def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
+    _check(y, "y", m * cin)
+    _check(dz, "dz", m * cout)
+    _check(dpk, "d_pointwise_kernel", cin * cout)
+    ws, wsb = _ws(L.query("unet_pointwise_bwd_filter_workspace", m, cin, cout), y.device)
+    _call("unet_pointwise_bwd_filter", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(y),
+          _ptr(dz), m, cin, cout, _ptr(dpk), ws, wsb, _stream())
+
+
+# ------------------------------------------------------------------ BatchNorm ---
+def bn_finalize(partials: Tensor, m: int, c: int, gamma, beta, eps, momentum, moving_mean, moving_var,
+                update_moving: bool, mean, rstd, scale, shift):
+    L.call("unet_bn_finalize", _ptr(partials), m, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+           _ptr(moving_mean), _ptr(moving_var), int(bool(update_moving)), _ptr(mean), _ptr(rstd), _ptr(scale),
+           _ptr(shift), _stream())
+
+
+def bn_infer_params(gamma, beta, moving_mean, moving_var, c: int, eps, scale: Tensor, shift: Tensor):
+    L.call("unet_bn_infer_params", _ptr(gamma), _ptr(beta), _ptr(moving_mean), _ptr(moving_var), c, float(eps),
+           _ptr(scale), _ptr(shift), _stream())
+
+
+def bn_relu_bwd(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, shift, use_bn: bool, drop_rate: float,
+                drop_seed: int, dgamma, dbeta, dz: Tensor):
+    _check(da, "da", m * c)
+    _check(z, "z", m * c)
+    _check(dz, "dz", m * c)
+    ws, wsb = _ws(L.query("unet_bn_relu_bwd_workspace", m, c), z.device)
+    L.call("unet_bn_relu_bwd", _ptr(da), _ptr(z), m, c, _ptr(mean), _ptr(rstd), _ptr(scale), _ptr(shift),
+           int(bool(use_bn)), float(drop_rate), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dgamma), _ptr(dbeta),
+           _ptr(dz), ws, wsb, _stream())
+
+
+# ------------------------------------------------------------ Conv2DTranspose ---
+def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor], out: Tensor):
+    _check(k, "kernel", 4 * cout * x.c0)
+    _check(out, "out", n * 4 * h * w * cout)
+    vs = x.c_struct()
+    m = n * h * w
+    _call("unet_conv_transpose2x2_fwd", (8.0 * m * x.c0 * cout, 4.0 * (m * x.c0 + 4 * m * cout + 4 * x.c0 * cout)),
+          ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(b), _ptr(out), _stream())
+
+
+def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Optional[Tensor], dk: Tensor,
+                          db: Tensor):
+    _check(dout, "dout", n * 4 * h * w * cout)
+    _check(dk, "dkernel", 4 * cout * x.c0)
+    _check(db, "dbias", cout)
+    if dx is not None:
+        _check(dx, "dx", n * h * w * x.c0)
+    ws, wsb = _ws(L.query("unet_conv_transpose2x2_bwd_workspace", n, h, w, x.c0, cout), dout.device)
+    vs = x.c_struct()
+    L.call("unet_conv_transpose2x2_bwd", ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(dout), _ptr(dx), _ptr(dk),
+           _ptr(db), ws, wsb, _stream())
+
+
+# ---------------------------------------------------------------- head / loss ---
+def head_fwd(x: View, n, h, w, ncls, k: Tensor, b: Optional[Tensor], prob: Tensor):
+    _check(k, "kernel", x.c0 * ncls)
+    _check(prob, "prob", n * h * w * ncls)
+    vs = x.c_struct()
+    L.call("unet_head_fwd", ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(b), _ptr(prob), _stream())
+
+
+def dice_fwd(y_true: Tensor, y_pred: Tensor, n: int, hw: int, ncls: int, smooth: float, sums: Optional[Tensor],
+             result: Tensor):
+    _check(y_true, "y_true", n * hw * ncls)
+    _check(y_pred, "y_pred", n * hw * ncls)
+    _check(result, "result", 3)
+    if sums is not None:
+        _check(sums, "sums", n * ncls * 3)
+    ws, wsb = _ws(L.query("unet_dice_workspace", n, hw, ncls), y_pred.device)
+    L.call("unet_dice_fwd", _ptr(y_true), _ptr(y_pred), n, hw, ncls, float(smooth), _ptr(sums), _ptr(result), ws,
+           wsb, _stream())
+
+
+def head_bwd(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, sums: Tensor, smooth: float,
+             loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor):
+    _check(prob, "prob", n * h * w * ncls)
+    _check(y_true, "y_true", n * h * w * ncls)
+    _check(dx, "dx", n * h * w * x.c0)
+    ws, wsb = _ws(L.query("unet_head_bwd_workspace", n, h, w, x.c0, ncls), prob.device)
+    vs = x.c_struct()
+    L.call("unet_head_bwd", ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums),
+           float(smooth), int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), ws, wsb, _stream())
+
+
+def meaniou_update(y_true: Tensor, y_pred: Tensor, num_classes: int, threshold: Optional[float],
+                   confusion: Tensor):
+    _check(y_true, "y_true")
+    _check(y_pred, "y_pred", y_true.numel())
+    if confusion.dtype != torch.int64 or confusion.numel() != num_classes * num_classes or not confusion.is_cuda:
+        raise ValueError("confusion: expected an int64 device tensor of num_classes^2 counts")
+    thr = -1.0 if threshold is None else float(threshold)
+    if threshold is not None and threshold < 0:
+        raise ValueError("threshold must be >= 0")
+    L.call("unet_meaniou_update", _ptr(y_true), _ptr(y_pred), y_true.numel(), num_classes, thr, _ptr(confusion),
+           _stream())
+
+
+def adamw_step(param: Tensor, grad: Tensor, m: Tensor, v: Tensor, lr, wd, b1, b2, eps, alpha, grad_scale=1.0):
+    n = param.numel()
+    for t, nm in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
+        _check(t, nm, n)
+    L.call("unet_adamw_step", _ptr(param), _ptr(grad), _ptr(m), _ptr(v), n, float(lr), float(wd), float(b1),
+           float(b2), float(eps), float(alpha), float(grad_scale), _stream())
