@@ -3,7 +3,10 @@ reference's builder API (model/u_net.py U_NET) and the train step of scripts/tra
 
 Tolerances (north star: masks within 1e-3 on identical weights/inputs):
   * inference probabilities: max |p - p_ref| < 1e-3 (measured ~1e-6);
-  * one train step: loss within 1e-5; every gradient tensor within 1e-3 relative L2 norm;
+  * one train step: loss within 1e-5; every gradient tensor within relative L2 norm
+    max(1e-3, 2 x e32) of the float64 oracle, where e32 is how far the SAME oracle run in
+    float32 lands from float64 for that tensor (the network's own fp32 conditioning: BN over
+    few samples at small test sizes amplifies rounding to ~1e-3..1e-2 in some gradients);
     post-AdamW weights within 1e-4 relative.
 """
 import numpy as np
@@ -91,7 +94,17 @@ def test_train_step_parity(ncls, use_bn, drop, loss):
                                                   loss="dice" if loss == "dice_loss" else "iou")
     assert abs(res[0] - lval) < 1e-5, (res[0], lval)
     assert abs(res[1] - dice) < 1e-5
-    bad = {k: norm_err(grads[k], g[k]) for k in g if norm_err(grads[k], g[k]) > 1e-3}
+    # fp32 conditioning reference: the same oracle step in float32
+    p32 = {k: v.astype(np.float32) for k, v in p.items()}
+    prob32, cache32, _ = orc.forward(p32, x, training=True, drop_seeds=seeds if drop > 0 else None)
+    _, dprob32 = orc.loss_and_dprob(y, prob32, "dice" if loss == "dice_loss" else "iou")
+    g32, _ = orc.backward(p32, cache32, dprob32)
+    bad = {}
+    for k in g:
+        e = norm_err(grads[k], g[k])
+        tol = max(1e-3, 2.0 * norm_err(g32[k], g[k]))
+        if e > tol:
+            bad[k] = (e, tol)
     assert not bad, bad
     assert set(g) == set(grads)
     for k, v in newp.items():
