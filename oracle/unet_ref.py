@@ -110,9 +110,17 @@ class UNetOracle:
         return prob, cache, new_stats
 
     # ------------------------------------------------------------------ backward ------
-    def backward(self, p, cache, dprob):
-        """Gradients of every trainable variable given dL/dprob."""
+    def backward(self, p, cache, dprob, trace=None):
+        """Gradients of every trainable variable given dL/dprob.  If `trace` is a dict it
+        receives the gradient w.r.t. each conv_block's output activation, keyed by block."""
         grads = {}
+        if trace is not None:
+            _bb = self._block_bwd
+
+            def _traced(p_, name, da, cache_, grads_, drop=None):
+                trace[name] = da
+                return _bb(p_, name, da, cache_, grads_, drop)
+            self._block_bwd = _traced
         enc, dec = _stages(self.filters)
         da, dkh, dbh = K.head_bwd(cache["head_x"], p["output_mask/kernel"], cache["prob"], dprob, self.num_classes)
         grads["output_mask/kernel"] = dkh
@@ -139,6 +147,8 @@ class UNetOracle:
             da = dskips[stage] + K.maxpool2_bwd(skip_a, da)
             da = self._block_bwd(p, f"{stage}_block2", da, cache, grads)
             da = self._block_bwd(p, f"{stage}_block1", da, cache, grads)
+        if trace is not None:
+            del self._block_bwd
         return grads, da
 
     # ---------------------------------------------------------------- train step ------

@@ -47,6 +47,23 @@ def _data(rng, n, h, w, ncls):
     return x, y
 
 
+def pool_tie_margin(cache, filters=4):
+    """Smallest relative gap between the largest and second-largest positive value of any 2x2
+    max-pool window of the encoder skips.  Below ~1e-5 the argmax - and so where MaxPoolGrad
+    routes the gradient - is decided by fp32 rounding, not by the math (a discontinuity no
+    fp32 implementation can match an fp64 oracle on)."""
+    m = np.inf
+    for s in range(1, filters + 1):
+        a = cache[f"enc{s}_skip"]
+        N, H, W, C = a.shape
+        w4 = np.sort(a.reshape(N, H // 2, 2, W // 2, 2, C).transpose(0, 1, 3, 5, 2, 4).reshape(-1, 4), axis=1)
+        top, second = w4[:, 3], w4[:, 2]
+        pos = top > 0
+        if pos.any():
+            m = min(m, float(((top - second)[pos] / top[pos]).min()))
+    return m
+
+
 def test_builder_api_and_inference_parity_cfg1():
     """configs[0]: U_NET((128,128,3), 1) forward on 2 images."""
     from model.u_net import U_NET, unet
@@ -76,18 +93,23 @@ def test_train_step_parity(ncls, use_bn, drop, loss):
     from unet_amd.optim import AdamW
     n, hw = 2, 32
     model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
-    rng = np.random.default_rng(ncls * 13 + int(drop * 10) + use_bn)
-    p = _weights_with_stats(model, rng)
-    x, y = _data(rng, n, hw, hw, ncls)
+    orc = UNetOracle(ncls, drop, use_bn)
+    seeds = model.engine.drop_seeds(1)
+    # precondition: no 2x2 max-pool window whose argmax is decided by rounding (see pool_tie_margin)
+    for attempt in range(20):
+        rng = np.random.default_rng(ncls * 13 + int(drop * 10) + use_bn + 1000 * attempt)
+        p = _weights_with_stats(model, rng)
+        x, y = _data(rng, n, hw, hw, ncls)
+        _, c0, _ = orc.forward(p, x.astype(np.float64), training=True, drop_seeds=seeds if drop > 0 else None)
+        if pool_tie_margin(c0) > 5e-6:
+            break
     lr, wd = 2e-3, 1e-4
     model.compile(AdamW(learning_rate=lr, weight_decay=wd), loss)
-    seeds = model.engine.drop_seeds(1)
     res = model.train_step(x, y).cpu().numpy()
     torch.cuda.synchronize()
     grads = {k: host(t) for k, t in model.engine.gvars.items()}
     neww = model.engine.get_weights_dict()
 
-    orc = UNetOracle(ncls, drop, use_bn)
     opt = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in p.items() if k in grads}
     lval, dice, g, newp, _, prob = orc.train_step(p, opt, x.astype(np.float64), y.astype(np.float64), 1, lr, wd,
                                                   drop_seeds=seeds if drop > 0 else None,
@@ -100,12 +122,18 @@ def test_train_step_parity(ncls, use_bn, drop, loss):
     _, dprob32 = orc.loss_and_dprob(y, prob32, "dice" if loss == "dice_loss" else "iou")
     g32, _ = orc.backward(p32, cache32, dprob32)
     bad = {}
+    rows = []
     for k in g:
         e = norm_err(grads[k], g[k])
-        tol = max(1e-3, 2.0 * norm_err(g32[k], g[k]))
+        e32 = norm_err(g32[k], g[k])
+        tol = max(1e-3, 2.0 * e32)
+        rows.append((e, e32, k))
         if e > tol:
             bad[k] = (e, tol)
-    assert not bad, bad
+    if bad:
+        for e, e32, k in sorted(rows, reverse=True)[:25]:
+            print(f"{k:45s} hip {e:.3e}  fp32-oracle {e32:.3e}")
+    assert not bad, sorted(bad.items())[:6]
     assert set(g) == set(grads)
     for k, v in newp.items():
         assert rel_err(neww[k], v) < 1e-4, k

@@ -15,11 +15,12 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__device__ __forceinline__ void decompose(int64_t p, int H, int W, int& n, int& h, int& w) {
-    w = (int)(p % W);
-    int64_t t = p / W;
-    h = (int)(t % H);
-    n = (int)(t / H);
+// 32-bit index math (the launchers check that every tensor has < 2^31 elements)
+__device__ __forceinline__ void decompose(int p, int H, int W, int& n, int& h, int& w) {
+    w = p % W;
+    const int t = p / W;
+    h = t % H;
+    n = t / H;
 }
 
 template <int MODE, bool DROP>
@@ -49,11 +50,10 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(DView v, int N, int H,
                                                           float* __restrict__ Y) {
     const int C = v.C;
     const int CQ = VEC ? C / 4 : C;
-    const int64_t total = (int64_t)N * H * W * CQ;
-    for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * kThreads) {
-        const int cq = (int)(idx % CQ);
-        const int64_t p = idx / CQ;
+    const int total = N * H * W * CQ;
+    for (int idx = blockIdx.x * kThreads + threadIdx.x; idx < total; idx += gridDim.x * kThreads) {
+        const int cq = idx % CQ;
+        const int p = idx / CQ;
         int n, h, w;
         decompose(p, H, W, n, h, w);
         if constexpr (VEC) {
@@ -100,11 +100,10 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_data_kernel(DView v, int N, i
                                                                float* __restrict__ dx1) {
     const int C = v.C;
     const int CQ = VEC ? C / 4 : C;
-    const int64_t total = (int64_t)N * H * W * CQ;
-    for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * kThreads) {
-        const int cq = (int)(idx % CQ);
-        const int64_t p = idx / CQ;
+    const int total = N * H * W * CQ;
+    for (int idx = blockIdx.x * kThreads + threadIdx.x; idx < total; idx += gridDim.x * kThreads) {
+        const int cq = idx % CQ;
+        const int p = idx / CQ;
         int n, h, w;
         decompose(p, H, W, n, h, w);
         if constexpr (VEC) {
@@ -222,9 +221,9 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_filter_kernel(DView v, int N,
     const int cl = tid % CT;
     const int pl = tid / CT;
     const int cq = blockIdx.x * CT + cl;
-    const int64_t P = (int64_t)N * H * W;
-    const int64_t p0 = (int64_t)blockIdx.y * ppc;
-    const int64_t p1 = p0 + ppc < P ? p0 + ppc : P;
+    const int P = N * H * W;
+    const int p0 = blockIdx.y * (int)ppc;
+    const int p1 = p0 + (int)ppc < P ? p0 + (int)ppc : P;
     __shared__ float4 red[kThreads];
 
     const bool active = pl < PL && cq < CQ;
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_filter_kernel(DView v, int N,
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t] = f4(0.f);
     if (active) {
-        for (int64_t p = p0 + pl; p < p1; p += PL) {
+        for (int p = p0 + pl; p < p1; p += PL) {
             int n, h, w;
             decompose(p, H, W, n, h, w);
             if constexpr (VEC) {
@@ -290,11 +289,10 @@ __global__ __launch_bounds__(kThreads) void view_materialize_kernel(DView v, int
                                                                     float* __restrict__ out) {
     const int C = v.C;
     const int CQ = VEC ? C / 4 : C;
-    const int64_t total = (int64_t)N * H * W * CQ;
-    for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * kThreads) {
-        const int cq = (int)(idx % CQ);
-        const int64_t p = idx / CQ;
+    const int total = N * H * W * CQ;
+    for (int idx = blockIdx.x * kThreads + threadIdx.x; idx < total; idx += gridDim.x * kThreads) {
+        const int cq = idx % CQ;
+        const int p = idx / CQ;
         int n, h, w;
         decompose(p, H, W, n, h, w);
         if constexpr (VEC)
@@ -382,17 +380,34 @@ static bool view_vec(const unet_view* x) {
     return x->c0 % 4 == 0;
 }
 
+int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, float* Y, hipStream_t st);
+int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
+                      float* dx0, float* dx1, hipStream_t st);
+size_t dw_tiled_filter_partials(int N, int H, int W, int C);
+int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
+                        int* S_out, hipStream_t st);
+bool dw_tiled_ok(int C);
+
+static int check_dims(const unet_view* x, int n, int h, int w, const char* op) {
+    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "%s: bad shape n=%d h=%d w=%d", op, n, h, w);
+    const int64_t C = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
+    const int64_t src = (int64_t)n * h * w * C * (x->mode == UNET_VIEW_POOL_BNRELU ? 4 : 1);
+    UNET_CHECK_ARG(src < (int64_t(1) << 31), "%s: tensor too large for 32-bit indexing", op);
+    return 0;
+}
+
 }  // namespace unet
 
 using namespace unet;
 
 extern "C" int unet_dwconv3x3_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel, float* y,
                                   unet_stream_t stream) {
-    if (check_view(x, "unet_dwconv3x3_fwd")) return -1;
-    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "unet_dwconv3x3_fwd: bad shape n=%d h=%d w=%d", n, h, w);
+    if (check_view(x, "unet_dwconv3x3_fwd") || check_dims(x, n, h, w, "unet_dwconv3x3_fwd")) return -1;
     UNET_CHECK_ARG(dw_kernel && y, "unet_dwconv3x3_fwd: null kernel/output");
     const DView v = make_dview(*x);
     const bool vec = view_vec(x);
+    if (vec && dw_tiled_ok(v.C))
+        return dw_tiled_fwd(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, y, as_stream(stream));
     const int64_t work = (int64_t)n * h * w * (vec ? v.C / 4 : v.C);
     hipStream_t st = as_stream(stream);
     const int grid = grid_for(work);
@@ -402,8 +417,8 @@ extern "C" int unet_dwconv3x3_fwd(const unet_view* x, int n, int h, int w, const
 }
 
 extern "C" int unet_view_materialize(const unet_view* x, int n, int h, int w, float* out, unet_stream_t stream) {
-    if (check_view(x, "unet_view_materialize")) return -1;
-    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0 && out, "unet_view_materialize: bad args");
+    if (check_view(x, "unet_view_materialize") || check_dims(x, n, h, w, "unet_view_materialize")) return -1;
+    UNET_CHECK_ARG(out, "unet_view_materialize: null output");
     const DView v = make_dview(*x);
     const bool vec = view_vec(x);
     const int64_t work = (int64_t)n * h * w * (vec ? v.C / 4 : v.C);
@@ -416,12 +431,14 @@ extern "C" int unet_view_materialize(const unet_view* x, int n, int h, int w, fl
 
 extern "C" int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                                        const float* dy, float* dx0, float* dx1, unet_stream_t stream) {
-    if (check_view(x, "unet_dwconv3x3_bwd_data")) return -1;
-    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "unet_dwconv3x3_bwd_data: bad shape");
+    if (check_view(x, "unet_dwconv3x3_bwd_data") || check_dims(x, n, h, w, "unet_dwconv3x3_bwd_data")) return -1;
     UNET_CHECK_ARG(dw_kernel && dy && dx0, "unet_dwconv3x3_bwd_data: null pointer");
     UNET_CHECK_ARG(x->mode != UNET_VIEW_CONCAT || dx1, "unet_dwconv3x3_bwd_data: CONCAT view needs dx1");
     const DView v = make_dview(*x);
     const bool vec = view_vec(x);
+    if (vec && dw_tiled_ok(v.C))
+        return dw_tiled_bwd_data(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, dx1,
+                                 as_stream(stream));
     const int64_t work = (int64_t)n * h * w * (vec ? v.C / 4 : v.C);
     hipStream_t st = as_stream(stream);
     const int grid = grid_for(work);
@@ -432,19 +449,28 @@ extern "C" int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w, 
 
 extern "C" size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c) {
     if (n <= 0 || h <= 0 || w <= 0 || c <= 0) return 0;
+    if (dw_tiled_ok(c)) return align_up(dw_tiled_filter_partials(n, h, w, c) * sizeof(float), 256);
     FilterPlan fp = filter_plan(n, h, w, c);
     return align_up((size_t)fp.chunks * 9 * c * sizeof(float), 256);
 }
 
 extern "C" int unet_dwconv3x3_bwd_filter(const unet_view* x, int n, int h, int w, const float* dy,
                                          float* d_dw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
-    if (check_view(x, "unet_dwconv3x3_bwd_filter")) return -1;
-    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "unet_dwconv3x3_bwd_filter: bad shape");
+    if (check_view(x, "unet_dwconv3x3_bwd_filter") || check_dims(x, n, h, w, "unet_dwconv3x3_bwd_filter"))
+        return -1;
     UNET_CHECK_ARG(dy && d_dw_kernel, "unet_dwconv3x3_bwd_filter: null pointer");
     const DView v = make_dview(*x);
     const size_t need = unet_dwconv3x3_bwd_filter_workspace(n, h, w, v.C);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_dwconv3x3_bwd_filter: workspace %zu < %zu", ws_bytes, need);
     const bool vec = view_vec(x);
+    if (vec && dw_tiled_ok(v.C)) {
+        int S = 0;
+        float* part = static_cast<float*>(ws);
+        int rc = dw_tiled_bwd_filter(v, x->mode, x->drop_rate > 0.f, n, h, w, dy, part, &S, as_stream(stream));
+        if (rc) return rc;
+        return reduce_slabs(part, S, (int64_t)9 * v.C, d_dw_kernel, (int64_t)9 * v.C, (int64_t)9 * v.C,
+                            as_stream(stream));
+    }
     FilterPlan fp = filter_plan(n, h, w, v.C);
     hipStream_t st = as_stream(stream);
     dim3 grid(fp.ctiles, (unsigned)fp.chunks);

@@ -1,0 +1,352 @@
+// Tiled depthwise 3x3 kernels (the fast path of unet_dwconv3x3_*; reference op:
+// DepthwiseConv2dNative of SeparableConv2D, model/u_net.py:14-20).
+//
+// A block owns an 8 x TW pixel tile of one image and a chunk of 4*QT channels (TW = 256/QT,
+// so every lane owns one tile column x one channel quad).  The (8+2) x (TW+2) halo of the
+// input is staged into LDS ONCE, through the activation view (BN affine + ReLU, 2x2 max-pool,
+// concat, dropout are applied once per staged element instead of once per tap), then each
+// lane walks its column with a rolling 3-row register window: 3 ds_read_b128 per output
+// quad instead of 9.  HBM traffic ~ input x (1 + halo overhead) + output; the halo re-reads of
+// neighbouring tiles hit L2.  The weight gradient uses the same staging and accumulates the 9
+// tap sums in registers over a persistent loop of tiles, then one fixed-order LDS reduction
+// per block -> deterministic per-block partials.
+#include "view.h"
+
+namespace unet {
+
+int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, float* Y, hipStream_t st);
+int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
+                      float* dx0, float* dx1, hipStream_t st);
+size_t dw_tiled_filter_partials(int N, int H, int W, int C);
+int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
+                        int* S_out, hipStream_t st);
+bool dw_tiled_ok(int C);
+
+namespace {
+
+constexpr int TH = 8;
+
+template <int QT>
+struct Geom {
+    static constexpr int TW = 256 / QT;
+    static constexpr int HWp = TW + 2;
+    static constexpr int HHp = TH + 2;
+    static constexpr int NE = HHp * HWp * QT;
+};
+
+// halo tile rows h0-1..h0+TH, cols w0-1..w0+TW, channels [cbase, cbase + 4 QT), zero outside
+template <int MODE, bool DROP, int QT>
+__device__ __forceinline__ void stage(float4* T, const DView& v, int n, int h0, int w0, int H, int W, int cbase) {
+    using G = Geom<QT>;
+    for (int e = threadIdx.x; e < G::NE; e += 256) {
+        const int q = e % QT;
+        const int pix = e / QT;
+        const int r = pix / G::HWp;
+        const int cc = pix - r * G::HWp;
+        const int hh = h0 - 1 + r, ww = w0 - 1 + cc;
+        float4 val = f4(0.f);
+        if (hh >= 0 && hh < H && ww >= 0 && ww < W) {
+            const int c = cbase + 4 * q;
+            val = view_load4<MODE>(v, n, hh, ww, H, W, c);
+            if constexpr (DROP) {
+                const uint64_t i = ((uint64_t)((n * H + hh) * W + ww)) * v.C + c;
+                val.x *= drop_mult(v.seed, i + 0, v.rate, v.inv_keep);
+                val.y *= drop_mult(v.seed, i + 1, v.rate, v.inv_keep);
+                val.z *= drop_mult(v.seed, i + 2, v.rate, v.inv_keep);
+                val.w *= drop_mult(v.seed, i + 3, v.rate, v.inv_keep);
+            }
+        }
+        T[e] = val;
+    }
+}
+
+__device__ __forceinline__ void tile_coords(int b, int tiles_w, int tiles_h, int TW, int& n, int& h0, int& w0) {
+    const int tw = b % tiles_w;
+    b /= tiles_w;
+    const int th = b % tiles_h;
+    n = b / tiles_h;
+    h0 = th * TH;
+    w0 = tw * TW;
+}
+
+template <int MODE, bool DROP, int QT>
+__global__ __launch_bounds__(256) void dw_tile_fwd(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+                                                   const float* __restrict__ K, float* __restrict__ Y) {
+    using G = Geom<QT>;
+    __shared__ float4 T[G::NE];
+    int n, h0, w0;
+    tile_coords(blockIdx.x, tiles_w, tiles_h, G::TW, n, h0, w0);
+    const int cbase = blockIdx.y * 4 * QT;
+    stage<MODE, DROP, QT>(T, v, n, h0, w0, H, W, cbase);
+    const int q = threadIdx.x % QT, col = threadIdx.x / QT;
+    const int C = v.C, c = cbase + 4 * q;
+    float4 k[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) k[t] = ld4(K + t * C + c);
+    __syncthreads();
+    const int w = w0 + col;
+    float4 a[3][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i][j] = T[(i * G::HWp + col + j) * QT + q];
+#pragma unroll
+    for (int r = 0; r < TH; ++r) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
+        float4 acc = f4(0.f);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) acc = fma4(a[i][j], k[i * 3 + j], acc);
+        if (w < W && h0 + r < H) st4(Y + ((int64_t)(n * H + h0 + r) * W + w) * C + c, acc);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            a[0][j] = a[1][j];
+            a[1][j] = a[2][j];
+        }
+    }
+}
+
+template <int MODE, bool DROP, int QT>
+__global__ __launch_bounds__(256) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+                                                        const float* __restrict__ K, const float* __restrict__ dY,
+                                                        float* __restrict__ dx0, float* __restrict__ dx1) {
+    using G = Geom<QT>;
+    __shared__ float4 T[G::NE];
+    int n, h0, w0;
+    tile_coords(blockIdx.x, tiles_w, tiles_h, G::TW, n, h0, w0);
+    const int cbase = blockIdx.y * 4 * QT;
+    const int C = v.C;
+    DView dv{};
+    dv.src0 = dY;
+    dv.c0 = C;
+    dv.C = C;
+    stage<UNET_VIEW_PLAIN, false, QT>(T, dv, n, h0, w0, H, W, cbase);
+    const int q = threadIdx.x % QT, col = threadIdx.x / QT;
+    const int c = cbase + 4 * q;
+    float4 kf[9];  // flipped kernel: dx(h,w) = sum dy(h-i+1, w-j+1) k[i][j]
+#pragma unroll
+    for (int t = 0; t < 9; ++t) kf[t] = ld4(K + (8 - t) * C + c);
+    __syncthreads();
+    const int w = w0 + col;
+    float4 a[3][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[i][j] = T[(i * G::HWp + col + j) * QT + q];
+#pragma unroll
+    for (int r = 0; r < TH; ++r) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
+        float4 acc = f4(0.f);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) acc = fma4(a[i][j], kf[i * 3 + j], acc);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            a[0][j] = a[1][j];
+            a[1][j] = a[2][j];
+        }
+        const int h = h0 + r;
+        if (w >= W || h >= H) continue;
+        const int p = (n * H + h) * W + w;
+        if constexpr (DROP) {
+            const uint64_t li = (uint64_t)p * C + c;
+            acc.x *= drop_mult(v.seed, li + 0, v.rate, v.inv_keep);
+            acc.y *= drop_mult(v.seed, li + 1, v.rate, v.inv_keep);
+            acc.z *= drop_mult(v.seed, li + 2, v.rate, v.inv_keep);
+            acc.w *= drop_mult(v.seed, li + 3, v.rate, v.inv_keep);
+        }
+        if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
+            st4(dx0 + (int64_t)p * C + c, acc);
+        } else if constexpr (MODE == UNET_VIEW_CONCAT) {
+            if (c < v.c0)
+                st4(dx0 + (int64_t)p * v.c0 + c, acc);
+            else
+                st4(dx1 + (int64_t)p * v.c1 + (c - v.c0), acc);
+        } else {  // POOL_BNRELU: gradient to the first max of the 2x2 window, accumulated
+            const int W2 = 2 * W;
+            const int64_t b = ((int64_t)(n * 2 * H + 2 * h) * W2 + 2 * w) * v.c0 + c;
+            const int64_t off[4] = {0, v.c0, (int64_t)W2 * v.c0, (int64_t)W2 * v.c0 + v.c0};
+            const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
+            float4 xv[4], g[4];
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                xv[qq] = bnrelu4(ld4(v.src0 + b + off[qq]), sc, sh);
+                g[qq] = ld4(dx0 + b + off[qq]);
+            }
+#define UNET_ROUTE(comp)                                                   \
+    {                                                                      \
+        float best = xv[0].comp;                                           \
+        int arg = 0;                                                       \
+        if (xv[1].comp > best) { best = xv[1].comp; arg = 1; }             \
+        if (xv[2].comp > best) { best = xv[2].comp; arg = 2; }             \
+        if (xv[3].comp > best) { best = xv[3].comp; arg = 3; }             \
+        g[0].comp += arg == 0 ? acc.comp : 0.f;                            \
+        g[1].comp += arg == 1 ? acc.comp : 0.f;                            \
+        g[2].comp += arg == 2 ? acc.comp : 0.f;                            \
+        g[3].comp += arg == 3 ? acc.comp : 0.f;                            \
+    }
+            UNET_ROUTE(x)
+            UNET_ROUTE(y)
+            UNET_ROUTE(z)
+            UNET_ROUTE(w)
+#undef UNET_ROUTE
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) st4(dx0 + b + off[qq], g[qq]);
+        }
+    }
+}
+
+template <int MODE, bool DROP, int QT>
+__global__ __launch_bounds__(256) void dw_tile_bwd_filter(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+                                                          int ntiles, const float* __restrict__ dY,
+                                                          float* __restrict__ part) {
+    using G = Geom<QT>;
+    __shared__ float4 T[G::NE];
+    const int cbase = blockIdx.y * 4 * QT;
+    const int C = v.C;
+    const int q = threadIdx.x % QT, col = threadIdx.x / QT;
+    const int c = cbase + 4 * q;
+    float4 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f4(0.f);
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        int n, h0, w0;
+        tile_coords(tile, tiles_w, tiles_h, G::TW, n, h0, w0);
+        __syncthreads();  // previous tile's readers are done with T
+        stage<MODE, DROP, QT>(T, v, n, h0, w0, H, W, cbase);
+        __syncthreads();
+        const int w = w0 + col;
+        float4 a[3][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a[i][j] = T[(i * G::HWp + col + j) * QT + q];
+#pragma unroll
+        for (int r = 0; r < TH; ++r) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
+            const int h = h0 + r;
+            const float4 g = (w < W && h < H) ? ld4(dY + ((int64_t)(n * H + h) * W + w) * C + c) : f4(0.f);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[i * 3 + j] = fma4(a[i][j], g, acc[i * 3 + j]);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                a[0][j] = a[1][j];
+                a[1][j] = a[2][j];
+            }
+        }
+    }
+    // fixed-order reduction over the TW column lanes of each channel quad
+    float* out = part + (int64_t)blockIdx.x * 9 * C;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        __syncthreads();
+        T[threadIdx.x] = acc[t];
+        __syncthreads();
+        if (col == 0) {
+            float4 s = T[q];
+            for (int cl = 1; cl < G::TW; ++cl) s = add4(s, T[cl * QT + q]);
+            st4(out + t * C + c, s);
+        }
+    }
+}
+
+int qt_for(int C) {
+    if (C % 4) return 0;
+    if (C % 64 == 0) return 16;
+    const int q = C / 4;
+    return (q == 1 || q == 2 || q == 4 || q == 8) ? q : 0;
+}
+
+struct TilePlan {
+    int qt, tw, tiles_w, tiles_h, chunks, ntiles;
+};
+TilePlan tile_plan(int N, int H, int W, int C) {
+    TilePlan p;
+    p.qt = qt_for(C);
+    p.tw = p.qt ? 256 / p.qt : 1;
+    p.tiles_w = (int)cdiv(W, p.tw);
+    p.tiles_h = (int)cdiv(H, TH);
+    p.chunks = p.qt ? C / (4 * p.qt) : 1;
+    p.ntiles = N * p.tiles_w * p.tiles_h;
+    return p;
+}
+int filter_blocks(const TilePlan& p) {
+    int g = (int)cdiv(1024, p.chunks);
+    if (g > p.ntiles) g = p.ntiles;
+    if (g < 1) g = 1;
+    return g;
+}
+
+#define UNET_TILE_DISPATCH_QT(KERNEL, MODE, DROP, GRID, ...)                       \
+    switch (p.qt) {                                                                \
+        case 16: KERNEL<MODE, DROP, 16><<<GRID, 256, 0, st>>>(__VA_ARGS__); break; \
+        case 8: KERNEL<MODE, DROP, 8><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
+        case 4: KERNEL<MODE, DROP, 4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
+        case 2: KERNEL<MODE, DROP, 2><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
+        default: KERNEL<MODE, DROP, 1><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;  \
+    }
+#define UNET_TILE_DISPATCH(KERNEL, GRID, ...)                                                       \
+    switch (mode) {                                                                                 \
+        case UNET_VIEW_PLAIN:                                                                       \
+            if (drop) { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_PLAIN, true, GRID, __VA_ARGS__) }    \
+            else { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_PLAIN, false, GRID, __VA_ARGS__) }        \
+            break;                                                                                  \
+        case UNET_VIEW_BNRELU:                                                                      \
+            if (drop) { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_BNRELU, true, GRID, __VA_ARGS__) }   \
+            else { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_BNRELU, false, GRID, __VA_ARGS__) }       \
+            break;                                                                                  \
+        case UNET_VIEW_POOL_BNRELU:                                                                 \
+            if (drop) { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_POOL_BNRELU, true, GRID, __VA_ARGS__) } \
+            else { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_POOL_BNRELU, false, GRID, __VA_ARGS__) }  \
+            break;                                                                                  \
+        default:                                                                                    \
+            if (drop) { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_CONCAT, true, GRID, __VA_ARGS__) }   \
+            else { UNET_TILE_DISPATCH_QT(KERNEL, UNET_VIEW_CONCAT, false, GRID, __VA_ARGS__) }       \
+            break;                                                                                  \
+    }
+
+}  // namespace
+
+bool dw_tiled_ok(int C) { return qt_for(C) != 0; }
+
+int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, float* Y, hipStream_t st) {
+    TilePlan p = tile_plan(N, H, W, v.C);
+    dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
+    UNET_TILE_DISPATCH(dw_tile_fwd, grid, v, N, H, W, p.tiles_w, p.tiles_h, K, Y)
+    UNET_CHECK_LAUNCH("dwconv3x3_fwd(tiled)");
+    return 0;
+}
+
+int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
+                      float* dx0, float* dx1, hipStream_t st) {
+    TilePlan p = tile_plan(N, H, W, v.C);
+    dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
+    UNET_TILE_DISPATCH(dw_tile_bwd_data, grid, v, N, H, W, p.tiles_w, p.tiles_h, K, dY, dx0, dx1)
+    UNET_CHECK_LAUNCH("dwconv3x3_bwd_data(tiled)");
+    return 0;
+}
+
+size_t dw_tiled_filter_partials(int N, int H, int W, int C) {
+    TilePlan p = tile_plan(N, H, W, C);
+    return (size_t)filter_blocks(p) * 9 * C;
+}
+
+int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
+                        int* S_out, hipStream_t st) {
+    TilePlan p = tile_plan(N, H, W, v.C);
+    const int G = filter_blocks(p);
+    dim3 grid((unsigned)G, (unsigned)p.chunks);
+    UNET_TILE_DISPATCH(dw_tile_bwd_filter, grid, v, N, H, W, p.tiles_w, p.tiles_h, p.ntiles, dY, part)
+    UNET_CHECK_LAUNCH("dwconv3x3_bwd_filter(tiled)");
+    *S_out = G;
+    return 0;
+}
+
+}  // namespace unet
