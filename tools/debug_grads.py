@@ -29,3 +29,6 @@ for b in model.engine.blocks:
     print(f"{b.name:15s} dA err {norm_err(hda, trace[b.name]):.3e}   |dA| {np.linalg.norm(trace[b.name]):.3e}")
 for k in ("enc2_block2_bn/gamma", "enc2_block2_sepconv/pointwise_kernel", "enc2_block1_bn/gamma"):
     print(k, norm_err(model.engine.gvars[k].cpu().numpy(), g[k]))
+errs = sorted(((norm_err(model.engine.gvars[k].cpu().numpy(), g[k]), k) for k in g))
+print("smallest:", errs[:5])
+print("largest:", errs[-5:])

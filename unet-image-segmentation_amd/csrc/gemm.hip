@@ -411,10 +411,419 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
         }
 }
 
+// ---------------------------------------------------------------- vectorised rows GEMM ----
+// As[m][BK+4], Bs[n][BK+4] (k contiguous).  In a group of 8 k, MFMA step s takes k-slot 0 =
+// k0+s and k-slot 1 = k0+4+s, so lane (row, half) feeds 4 consecutive MFMAs from ONE
+// ds_read_b128 of its row.  Row stride BK+4 floats makes those reads conflict-free.
+template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI>
+__global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
+    constexpr int LR = BK + 4;
+    constexpr int KQ = BK / 4;
+    constexpr int AQ = BM * KQ / 256;
+    constexpr int BQ = BN * KQ / 256;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    __shared__ __attribute__((aligned(16))) float As[2][BM * LR];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LR];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int M_rem = (g.M - m0) < BM ? (int)(g.M - m0) : BM;
+
+    // A: this thread stages k-quad kq of rows arow + (256/KQ) r
+    const int kq = tid % KQ;
+    const int arow = tid / KQ;
+    int aoff[AQ];
+#pragma unroll
+    for (int r = 0; r < AQ; ++r) {
+        const int rr = arow + (256 / KQ) * r;
+        if (rr < M_rem) {
+            const int m = m0 + rr;
+            if constexpr (AMODE == A_UNSHUFFLE) {
+                const int hw = g.uH * g.uW;
+                const int n = m / hw;
+                const int rem = m - n * hw;
+                const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
+                aoff[r] = ((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf;
+            } else {
+                aoff[r] = m * g.a.c0;
+            }
+        } else {
+            aoff[r] = -1;
+        }
+    }
+    // B: k-contiguous (bkc) -> quads along k of columns; else quads along n of k-rows
+    const bool bkc = g.sbk == 1;
+    constexpr int NQ = BN / 4;
+    const int bkq = tid % KQ, bcol = tid / KQ;     // bkc mapping
+    const int bnq = tid % NQ, bkrow = tid / NQ;    // n-contiguous mapping
+
+    float4 ra[AQ], rb[BQ];
+    auto load_stage = [&](int k0) {
+        const int k = k0 + 4 * kq;
+        const bool kv = k < g.K;
+        int koff = k;
+        float4 sc = f4(1.f), sh = f4(0.f);
+        if constexpr (AMODE == A_UNSHUFFLE) {
+            const int ab = k / g.uf;
+            const int co = k - ab * g.uf;
+            koff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
+        }
+        if constexpr (AMODE == A_BNRELU) {
+            if (kv) {
+                sc = ld4(g.a.sc0 + k);
+                sh = ld4(g.a.sh0 + k);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < AQ; ++r) {
+            float4 v = f4(0.f);
+            if (kv && aoff[r] >= 0) {
+                v = ld4(g.a.src0 + aoff[r] + koff);
+                if constexpr (AMODE == A_BNRELU) v = bnrelu4(v, sc, sh);
+                if constexpr (DROP) {
+                    const uint64_t i = (uint64_t)(m0 + arow + (256 / KQ) * r) * g.a.C + k;
+                    v.x *= drop_mult(g.a.seed, i + 0, g.a.rate, g.a.inv_keep);
+                    v.y *= drop_mult(g.a.seed, i + 1, g.a.rate, g.a.inv_keep);
+                    v.z *= drop_mult(g.a.seed, i + 2, g.a.rate, g.a.inv_keep);
+                    v.w *= drop_mult(g.a.seed, i + 3, g.a.rate, g.a.inv_keep);
+                }
+            }
+            ra[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < BQ; ++r) {
+            float4 v = f4(0.f);
+            if (bkc) {
+                const int n = n0 + bcol + (256 / KQ) * r, kk = k0 + 4 * bkq;
+                if (n < g.N && kk < g.K) v = ld4(g.B + (int64_t)n * g.sbn + kk);
+            } else {
+                const int kk = k0 + bkrow + (256 / NQ) * r, n = n0 + 4 * bnq;
+                if (n < g.N && kk < g.K) v = ld4(g.B + (int64_t)kk * g.sbk + n);
+            }
+            rb[r] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < AQ; ++r)
+            *reinterpret_cast<float4*>(&As[buf][(arow + (256 / KQ) * r) * LR + 4 * kq]) = ra[r];
+#pragma unroll
+        for (int r = 0; r < BQ; ++r) {
+            if (bkc) {
+                *reinterpret_cast<float4*>(&Bs[buf][(bcol + (256 / KQ) * r) * LR + 4 * bkq]) = rb[r];
+            } else {
+                const int kk = bkrow + (256 / NQ) * r, nn = 4 * bnq;
+                Bs[buf][(nn + 0) * LR + kk] = rb[r].x;
+                Bs[buf][(nn + 1) * LR + kk] = rb[r].y;
+                Bs[buf][(nn + 2) * LR + kk] = rb[r].z;
+                Bs[buf][(nn + 3) * LR + kk] = rb[r].w;
+            }
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+    const int nk = (g.K + BK - 1) / BK;
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage((kt + 1) * BK);
+#pragma unroll
+        for (int kg = 0; kg < BK / 8; ++kg) {
+            float4 af[TM], bf[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+                af[tm] = *reinterpret_cast<const float4*>(&As[buf][(wm * (BM / 2) + tm * 32 + lo) * LR + kg * 8 + 4 * hi]);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                bf[tn] = *reinterpret_cast<const float4*>(&Bs[buf][(wn * (BN / 2) + tn * 32 + lo) * LR + kg * 8 + 4 * hi]);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].x, bf[tn].x, acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].y, bf[tn].y, acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].z, bf[tn].z, acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].w, bf[tn].w, acc[tm][tn], 0, 0, 0);
+                }
+        }
+        if (kt + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+
+    if constexpr (EPI == E_STORE || EPI == E_STATS) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
+                if (n >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
+                    if (rr < M_rem) g.C[(int64_t)(m0 + rr) * g.ldc + n] = acc[tm][tn][r];
+                }
+            }
+    }
+    if constexpr (EPI == E_STATS) {
+        float* red = &As[0][0];
+        float mean[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            float s = 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) s += acc[tm][tn][r];
+            s += __shfl_xor(s, 32, 64);
+            if (hi == 0) red[wm * BN + col] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            mean[tn] = (red[col] + red[BN + col]) / (float)M_rem;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            float q = 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) {
+                        const float d = acc[tm][tn][r] - mean[tn];
+                        q = fmaf(d, d, q);
+                    }
+            q += __shfl_xor(q, 32, 64);
+            if (hi == 0) red[wm * BN + col] = q;
+        }
+        __syncthreads();
+        if (wm == 0 && hi == 0) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * (BN / 2) + tn * 32 + lo;
+                const int n = n0 + col;
+                if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = make_float2(mean[tn], red[col] + red[BN + col]);
+            }
+        }
+    }
+    if constexpr (EPI == E_SHUFFLE) {
+        const int hw = g.sH * g.sW;
+        int obase[TM][16];  // output pixel offset (a = b = 0 tap) of each accumulator row
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
+                const int m = m0 + rr;
+                const int img = m / hw;
+                const int rem = m - img * hw;
+                const int i = rem / g.sW, j = rem - (rem / g.sW) * g.sW;
+                obase[tm][r] = rr < M_rem ? ((img * 2 * g.sH + 2 * i) * (2 * g.sW) + 2 * j) * g.sf : -1;
+            }
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
+            if (n >= g.N) continue;
+            const int ab = n / g.sf;
+            const int co = n - ab * g.sf;
+            const int toff = (ab >> 1) * (2 * g.sW * g.sf) + (ab & 1) * g.sf + co;
+            const float bias = g.bias ? g.bias[co] : 0.f;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (obase[tm][r] >= 0) g.C[(int64_t)obase[tm][r] + toff] = acc[tm][tn][r] + bias;
+        }
+    }
+}
+
+// ------------------------------------------------------------- vectorised wgrad GEMM ----
+template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
+__global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
+    constexpr int LDA = BP + 4, LDB = BQ + 4;
+    constexpr int TM = BP / 64, TN = BQ / 64;
+    constexpr int PQ = BP / 4, QQ = BQ / 4;          // quads per m-row
+    constexpr int AR = BK * PQ / 256, BR = BK * QQ / 256;
+    constexpr int AS = 256 / PQ, BS = 256 / QQ;      // m-row step between a thread's quads
+    __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wp = wave >> 1, wq = wave & 1;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int ntp = (g.P + BP - 1) / BP;
+    const int p0 = (blockIdx.x % ntp) * BP;
+    const int q0 = (blockIdx.x / ntp) * BQ;
+    const int mb = (int)(blockIdx.y * g.mslice);
+    const int me = (int)((mb + g.mslice) < g.M ? (mb + g.mslice) : g.M);
+
+    const int apq = tid % PQ, amm = tid / PQ;
+    const int p = p0 + 4 * apq;
+    const bool pv = p < g.P;
+    float4 asc = f4(1.f), ash = f4(0.f);
+    int poff = p;
+    if constexpr (AMODE == W_BNRELU) {
+        if (pv) {
+            asc = ld4(g.a.sc0 + p);
+            ash = ld4(g.a.sh0 + p);
+        }
+    }
+    if constexpr (AMODE == W_UNSHUFFLE) {
+        const int ab = p / g.uf;
+        const int co = p - ab * g.uf;
+        poff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
+    }
+    const int bqq = tid % QQ, bmm = tid / QQ;
+    const int q = q0 + 4 * bqq;
+    const bool qv = q < g.Q;
+    float4 bsc = f4(1.f), bsh = f4(0.f);
+    if constexpr (BMODE == W_BNRELU) {
+        if (qv) {
+            bsc = ld4(g.b.sc0 + q);
+            bsh = ld4(g.b.sh0 + q);
+        }
+    }
+
+    float4 ra[AR], rb[BR];
+    auto load_stage = [&](int k0) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) {
+            const int m = k0 + amm + AS * r;
+            float4 v = f4(0.f);
+            if (pv && m < me) {
+                if constexpr (AMODE == W_UNSHUFFLE) {
+                    const int hw = g.uH * g.uW;
+                    const int n = m / hw;
+                    const int rem = m - n * hw;
+                    const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
+                    v = ld4(g.a.src0 + ((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf + poff);
+                } else {
+                    v = ld4(g.a.src0 + (int64_t)m * g.a.c0 + p);
+                    if constexpr (AMODE == W_BNRELU) v = bnrelu4(v, asc, ash);
+                    if constexpr (ADROP) {
+                        const uint64_t i = (uint64_t)m * g.a.C + p;
+                        v.x *= drop_mult(g.a.seed, i + 0, g.a.rate, g.a.inv_keep);
+                        v.y *= drop_mult(g.a.seed, i + 1, g.a.rate, g.a.inv_keep);
+                        v.z *= drop_mult(g.a.seed, i + 2, g.a.rate, g.a.inv_keep);
+                        v.w *= drop_mult(g.a.seed, i + 3, g.a.rate, g.a.inv_keep);
+                    }
+                }
+            }
+            ra[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+            const int m = k0 + bmm + BS * r;
+            float4 v = f4(0.f);
+            if (qv && m < me) {
+                v = ld4(g.b.src0 + (int64_t)m * g.b.c0 + q);
+                if constexpr (BMODE == W_BNRELU) v = bnrelu4(v, bsc, bsh);
+                if constexpr (BDROP) {
+                    const uint64_t i = (uint64_t)m * g.b.C + q;
+                    v.x *= drop_mult(g.b.seed, i + 0, g.b.rate, g.b.inv_keep);
+                    v.y *= drop_mult(g.b.seed, i + 1, g.b.rate, g.b.inv_keep);
+                    v.z *= drop_mult(g.b.seed, i + 2, g.b.rate, g.b.inv_keep);
+                    v.w *= drop_mult(g.b.seed, i + 3, g.b.rate, g.b.inv_keep);
+                }
+            }
+            rb[r] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[buf][(amm + AS * r) * LDA + 4 * apq]) = ra[r];
+#pragma unroll
+        for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[buf][(bmm + BS * r) * LDB + 4 * bqq]) = rb[r];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+    const int nk = (me - mb + BK - 1) / BK;
+    if (nk > 0) {
+        load_stage(mb);
+        store_stage(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage(mb + (kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) av[tm] = As[buf][(2 * kk + hi) * LDA + wp * (BP / 2) + tm * 32 + lo];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bv[tn] = Bs[buf][(2 * kk + hi) * LDB + wq * (BQ / 2) + tn * 32 + lo];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+    float* slab = g.slab + (int64_t)blockIdx.y * g.P * g.Q;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int qq = q0 + wq * (BQ / 2) + tn * 32 + lo;
+            if (qq >= g.Q) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pp = p0 + wp * (BP / 2) + tm * 32 + acc_row(r, hi);
+                if (pp < g.P) slab[(int64_t)pp * g.Q + qq] = acc[tm][tn][r];
+            }
+        }
+}
+
 // ------------------------------------------------------------------------------ launchers ----
+bool rows_vec_ok(const RowsArgs& a, int amode) {
+    if (a.K % 4 || a.N % 4) return false;
+    if (amode == A_UNSHUFFLE && a.uf % 4) return false;
+    if (amode != A_UNSHUFFLE && a.a.c0 % 4) return false;
+    if (a.sbk != 1 && a.sbn != 1) return false;
+    return ((uintptr_t)a.a.src0 | (uintptr_t)a.B) % 16 == 0;
+}
+
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     const unsigned gm = (unsigned)cdiv(a.M, 128);
+    if (rows_vec_ok(a, AMODE)) {
+        if (a.N <= 64) {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 64));
+            gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+        } else {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 128));
+            gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+        }
+        UNET_CHECK_LAUNCH(what);
+        return 0;
+    }
     if (a.N <= 64) {
         dim3 grid(gm, (unsigned)cdiv(a.N, 64));
         gemm_rows_kernel<128, 64, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
@@ -448,6 +857,20 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
 template <int AMODE, bool ADROP, int BMODE, bool BDROP>
 void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
     dim3 grid((unsigned)w.tiles, (unsigned)w.S);
+    const bool vec = a.P % 4 == 0 && a.Q % 4 == 0 && (AMODE != W_UNSHUFFLE || a.uf % 4 == 0) &&
+                     (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
+                     ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
+    if (vec) {
+        if (w.bp == 128 && w.bq == 128)
+            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        else if (w.bp == 128)
+            gemm_wgrad_vec<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        else if (w.bq == 128)
+            gemm_wgrad_vec<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        else
+            gemm_wgrad_vec<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        return;
+    }
     if (w.bp == 128 && w.bq == 128)
         gemm_wgrad_kernel<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
     else if (w.bp == 128)
