@@ -1,0 +1,115 @@
+"""Generates tests/golden/*.npz from the NumPy oracle (oracle/).  Inputs and weights come from
+the portable splitmix64 stream (unet_amd.params.portable_uniform), so every vector here can be
+regenerated bit-for-bit; outputs are float64 oracle results stored as float32/float64.
+
+The reference itself ships no golden data and cannot run here (TensorFlow absent), so these
+fixtures freeze the oracle (parity unpinned against TF), they do not pin it.
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "unet-image-segmentation_amd"), ROOT]
+
+from oracle import keras_ops as K  # noqa: E402
+from oracle.unet_ref import UNetOracle  # noqa: E402
+from unet_amd.params import init_weights, portable_uniform, unet_variables  # noqa: E402
+
+
+def U(seed, shape, lo=0.0, hi=1.0):
+    n = int(np.prod(shape))
+    return (lo + (hi - lo) * portable_uniform(seed, n)).reshape(shape).astype(np.float32).astype(np.float64)
+
+
+def model_weights(ncls, filters, seed):
+    specs = unet_variables(3, ncls, True, filters)
+    w = {k: v.astype(np.float64) for k, v in init_weights(specs, seed).items()}
+    for i, k in enumerate(sorted(w)):
+        if k.endswith("moving_mean"):
+            w[k] = U(seed + 100 + i, w[k].shape, -0.2, 0.2)
+        elif k.endswith("moving_variance"):
+            w[k] = U(seed + 100 + i, w[k].shape, 0.5, 1.5)
+        elif k.endswith("gamma"):
+            w[k] = U(seed + 100 + i, w[k].shape, 0.7, 1.3)
+        elif k.endswith("beta"):
+            w[k] = U(seed + 100 + i, w[k].shape, -0.1, 0.1)
+    return w
+
+
+def ops_fixture():
+    out = {}
+    x = U(1, (2, 8, 8, 16), -1, 1)
+    dk = U(2, (3, 3, 16, 1), -1, 1)
+    dy = U(3, (2, 8, 8, 16), -1, 1)
+    out.update(dw_x=x, dw_k=dk, dw_dy=dy, dw_y=K.depthwise3x3(x, dk))
+    out["dw_dx"], out["dw_dk"] = K.depthwise3x3_bwd(x, dk, dy)
+    pk = U(4, (1, 1, 16, 32), -0.3, 0.3)
+    z = K.pointwise(x, pk)
+    dz = U(5, z.shape, -1, 1)
+    out.update(pw_k=pk, pw_z=z, pw_dz=dz)
+    out["pw_dx"], out["pw_dk"] = K.pointwise_bwd(x, pk, dz)
+    gamma, beta = U(6, (32,), 0.5, 1.5), U(7, (32,), -0.2, 0.2)
+    bn_out, mean, var = K.bn_train(z, gamma, beta)
+    da = U(8, z.shape, -1, 1)
+    out.update(bn_gamma=gamma, bn_beta=beta, bn_out=bn_out, bn_mean=mean, bn_var=var, bn_da=da)
+    out["bn_dz"], out["bn_dgamma"], out["bn_dbeta"] = K.bn_relu_bwd(da, z, gamma, beta, mean, var)
+    a = K.relu(bn_out)
+    out["pool_out"] = K.maxpool2(a)
+    out["pool_dx"] = K.maxpool2_bwd(a, U(9, out["pool_out"].shape, -1, 1))
+    out["pool_dout"] = U(9, out["pool_out"].shape, -1, 1)
+    ck, cb = U(10, (2, 2, 8, 16), -0.3, 0.3), U(11, (8,), -0.1, 0.1)
+    co = K.conv_transpose2x2(x, ck, cb)
+    cdo = U(12, co.shape, -1, 1)
+    out.update(ct_k=ck, ct_b=cb, ct_out=co, ct_dout=cdo)
+    out["ct_dx"], out["ct_dk"], out["ct_db"] = K.conv_transpose2x2_bwd(x, ck, cdo)
+    yt = (U(13, (2, 8, 8, 1)) > 0.5).astype(np.float64)
+    yp = U(14, (2, 8, 8, 1))
+    out.update(dice_yt=yt, dice_yp=yp, dice_loss=K.dice_loss(yt, yp), dice_coef=K.dice_coef(yt, yp),
+               iou_coef=K.iou_coef(yt, yp), dice_grad=K.dice_loss_grad(yt, yp))
+    out["miou_cm_trunc"] = K.meaniou_confusion(yt, yp, 2)
+    out["miou_cm_thr"] = K.meaniou_confusion(yt, yp, 2, 0.5)
+    p, g, m, v = U(15, (100,), -1, 1), U(16, (100,), -0.1, 0.1), U(17, (100,), -0.01, 0.01), U(18, (100,), 0, 0.01)
+    out.update(adam_p=p, adam_g=g, adam_m=m, adam_v=v)
+    out["adam_p1"], out["adam_m1"], out["adam_v1"] = K.adamw_update(p, g, m, v, 3, 2e-3, 1e-4)
+    out["drop_mask"] = K.dropout_mult(2301, (2, 4, 4, 8), 0.2)
+    return out
+
+
+def cfg1_fixture():
+    """configs[0]: U_NET((128,128,3), 1) forward on 2 images (inference mode)."""
+    w = model_weights(1, (64, 128, 256, 512), 2301)
+    x = U(7, (2, 128, 128, 3))
+    prob, _, _ = UNetOracle(1).forward(w, x, training=False)
+    return {"x_seed": 7, "w_seed": 2301, "prob": prob.astype(np.float32)}
+
+
+def train_fixture():
+    """One train step (dropout 0) at 32x32, batch 2, full widths: loss, dice, per-tensor grad
+    norms, and post-AdamW values of a few tensors."""
+    w = model_weights(1, (64, 128, 256, 512), 11)
+    x = U(21, (2, 32, 32, 3))
+    y = (U(22, (2, 32, 32, 1)) > 0.6).astype(np.float64)
+    orc = UNetOracle(1, 0.0)
+    opt = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in w.items() if "moving" not in k}
+    loss, dice, g, newp, _, prob = orc.train_step(w, opt, x, y, 1, 2e-3, 1e-4)
+    out = {"x_seed": 21, "y_seed": 22, "w_seed": 11, "loss": loss, "dice": dice}
+    for k, v in g.items():
+        out["gnorm:" + k] = np.linalg.norm(v)
+    for k in ("output_mask/kernel", "dec1_block2_bn/gamma", "enc1_block1_sepconv/pointwise_kernel"):
+        out["new:" + k] = newp[k]
+    return out
+
+
+if __name__ == "__main__":
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops_fixture())
+    np.savez_compressed(os.path.join(HERE, "cfg1_forward.npz"), **cfg1_fixture())
+    tf = train_fixture()
+    np.savez_compressed(os.path.join(HERE, "train_step.npz"), **{k.replace("/", "|"): v for k, v in tf.items()})
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -1,0 +1,82 @@
+"""Committed golden vectors (tests/golden/, made by make_golden.py): the oracle must keep
+reproducing them (CPU), and the HIP path must match them (GPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import keras_ops as K
+from oracle.unet_ref import UNetOracle
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+import sys  # noqa: E402
+sys.path.insert(0, HERE)
+import make_golden as MG  # noqa: E402
+
+
+def _load(name):
+    with np.load(os.path.join(HERE, name), allow_pickle=False) as z:
+        return {k.replace("|", "/"): z[k] for k in z.files}
+
+
+def test_oracle_reproduces_op_goldens():
+    g = _load("ops.npz")
+    new = MG.ops_fixture()
+    assert set(g) == set(new)
+    for k in g:
+        assert np.allclose(new[k], g[k], rtol=1e-12, atol=1e-14), k
+
+
+def test_oracle_reproduces_cfg1_golden():
+    g = _load("cfg1_forward.npz")
+    new = MG.cfg1_fixture()
+    assert np.abs(new["prob"].astype(np.float64) - g["prob"]).max() < 1e-6
+
+
+def test_oracle_reproduces_train_golden():
+    g = _load("train_step.npz")
+    new = MG.train_fixture()
+    for k, v in g.items():
+        assert np.allclose(new[k], v, rtol=1e-9, atol=1e-15), k
+
+
+@pytest.mark.gpu
+def test_hip_matches_cfg1_golden():
+    """configs[0] through the reference builder API: masks within 1e-3 of the golden output."""
+    from model.u_net import U_NET
+    g = _load("cfg1_forward.npz")
+    model = U_NET((128, 128, 3), 1)
+    w = MG.model_weights(1, (64, 128, 256, 512), int(g["w_seed"]))
+    model.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+    x = MG.U(int(g["x_seed"]), (2, 128, 128, 3)).astype(np.float32)
+    prob = model.predict(x)
+    err = np.abs(prob.astype(np.float64) - g["prob"]).max()
+    assert err < 1e-3
+    assert err < 2e-5
+
+
+@pytest.mark.gpu
+def test_hip_matches_train_golden():
+    import torch
+    from unet_amd.model import UNetModel
+    from unet_amd.optim import AdamW
+    g = _load("train_step.npz")
+    m = UNetModel((32, 32, 3), 1, dropout_rate=0.0)
+    w = MG.model_weights(1, (64, 128, 256, 512), int(g["w_seed"]))
+    m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+    x = MG.U(int(g["x_seed"]), (2, 32, 32, 3)).astype(np.float32)
+    y = (MG.U(int(g["y_seed"]), (2, 32, 32, 1)) > 0.6).astype(np.float32)
+    m.compile(AdamW(2e-3, 1e-4), "dice_loss")
+    res = m.train_step(x, y).cpu().numpy()
+    torch.cuda.synchronize()
+    assert abs(res[0] - g["loss"]) < 1e-5 and abs(res[1] - g["dice"]) < 1e-5
+    for k, v in g.items():
+        if k.startswith("gnorm:"):
+            name = k[6:]
+            hn = float(np.linalg.norm(m.engine.gvars[name].cpu().numpy().astype(np.float64)))
+            assert abs(hn - v) <= 1e-3 * v + 1e-12, (name, hn, float(v))
+    neww = m.engine.get_weights_dict()
+    for k, v in g.items():
+        if k.startswith("new:"):
+            name = k[4:]
+            assert np.abs(neww[name] - v).max() <= 1e-4 * np.abs(v).max(), name
