@@ -208,12 +208,13 @@ class UNetModel:
     def save_weights(self, path: str):
         """Neutral weight file: .npz keyed by Keras weight names, Keras layouts."""
         w = self.engine.get_weights_dict()
-        np.savez(path, **{k.replace("/", ":"): v for k, v in w.items()})
+        with open(path, "wb") as f:  # exact path (the reference's --model-out may say .h5)
+            np.savez(f, **{k.replace("/", ":"): v for k, v in w.items()})
 
     save = save_weights
 
     def load_weights(self, path: str):
-        with np.load(path, allow_pickle=False) as z:
+        with open(path, "rb") as f, np.load(f, allow_pickle=False) as z:
             self.engine.set_weights_dict({k.replace(":", "/"): z[k] for k in z.files})
 
     def count_params(self) -> int:
