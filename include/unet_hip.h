@@ -115,6 +115,15 @@ int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
                               int cin, int cout, float* d_pw_kernel,
                               void* ws, size_t ws_bytes, unet_stream_t stream);
 
+/* Fused SeparableConv2D: depthwise 3x3 of the view -> pointwise 1x1 (+ BatchNorm partials as
+ * unet_pointwise_fwd), the depthwise result never leaving the chip except as the optional `y`
+ * (needed by the pointwise weight gradient in training; NULL for inference).  Supported when
+ * unet_sepconv_fwd_supported() says so (h % 8 == 0, w % 16 == 0, channels % 4 == 0).     */
+int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int w, int cout);
+int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                     int cout, const float* pw_kernel, float* y, float* z,
+                     float* bn_partials, unet_stream_t stream);
+
 /* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
  * momentum 0.99, epsilon 1e-3, biased batch variance for both the output
  * and the moving-variance update).  Training: reduces bn_partials into the

@@ -97,6 +97,12 @@ def test_builder_api_and_inference_parity_cfg1():
     # except where |p - 0.5| is below the numeric noise
     far = np.abs(ref - 0.5) > 1e-4
     assert np.array_equal((prob > 0.5)[far], (ref > 0.5)[far])
+    # the fused depthwise+pointwise kernel (used here at the 128x128 level) against the split path
+    model.engine.fuse_sepconv = "never"
+    prob_split = model.predict(x)
+    model.engine.fuse_sepconv = "always"
+    prob_fused = model.predict(x)
+    assert np.abs(prob_split - ref).max() < 2e-5 and np.abs(prob_fused - ref).max() < 2e-5
 
 
 @pytest.mark.parametrize("ncls,use_bn,drop,loss", [(1, True, 0.0, "dice_loss"), (1, True, 0.2, "dice_loss"),

@@ -300,3 +300,53 @@ def test_errors_are_loud(ops):
         ops.dwconv3x3_fwd(ops.View(1, x, 8), 1, 4, 4, torch.zeros(72, device="cuda"), torch.empty_like(x))
     with pytest.raises(ValueError):
         ops.dwconv3x3_fwd(ops.View.plain(x.cpu()), 1, 4, 4, torch.zeros(72), torch.empty_like(x))
+
+
+SEP_CASES = [
+    # mode, n, h, w, c0, c1, cout, drop
+    (0, 2, 16, 32, 16, 0, 64, 0.0),
+    (1, 2, 8, 16, 64, 0, 128, 0.0),
+    (1, 1, 16, 16, 128, 0, 96, 0.2),
+    (2, 2, 8, 16, 32, 0, 64, 0.0),
+    (3, 2, 8, 32, 32, 32, 64, 0.0),
+    (3, 1, 16, 16, 16, 16, 256, 0.2),
+    (1, 1, 8, 16, 8, 0, 8, 0.0),     # K tail (8 channels < 16-channel stage)
+]
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", SEP_CASES)
+@pytest.mark.parametrize("train", [True, False])
+def test_fused_sepconv(ops, mode, n, h, w, c0, c1, cout, drop, train):
+    rng = np.random.default_rng(100 + mode + cout)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = f32(rng.standard_normal((3, 3, C, 1)))
+    pk = f32(rng.standard_normal((1, 1, C, cout)) / np.sqrt(C))
+    v = _mk_view(ops, mode, t, drop, 77)
+    assert ops.sepconv_supported(v, n, h, w, cout)
+    m = n * h * w
+    y = torch.full((n, h, w, C), -7.0, device="cuda")
+    z = torch.empty((n, h, w, cout), device="cuda")
+    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    ops.sepconv_fwd(v, n, h, w, dev(dk), cout, dev(pk), y if train else None, z, part if train else None)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 77)
+    yr = K.depthwise3x3(xv, dk)
+    zr = K.pointwise(yr, pk)
+    assert rel_err(host(z), zr) < 5e-6
+    if train:
+        assert rel_err(host(y), yr) < 2e-6
+        outs = [torch.empty(cout, device="cuda") for _ in range(4)]
+        gamma, beta = bn_affine(rng, cout)
+        ops.bn_finalize(part, m, cout, dev(gamma), dev(beta), 1e-3, 0.99, None, None, False, *outs)
+        _, mean, var = K.bn_train(zr, gamma, beta)
+        assert rel_err(host(outs[0]), mean) < 1e-4
+        assert rel_err(host(outs[1]), 1 / np.sqrt(var + 1e-3)) < 1e-5
+    else:
+        assert float(y.min()) == -7.0 and float(y.max()) == -7.0  # inference leaves y untouched
+
+
+def test_fused_sepconv_unsupported_shapes(ops):
+    x = torch.zeros((1, 8, 8, 16), device="cuda")
+    assert not ops.sepconv_supported(ops.View.plain(x), 1, 8, 8, 64)     # w % 16 != 0
+    x3 = torch.zeros((1, 16, 16, 3), device="cuda")
+    assert not ops.sepconv_supported(ops.View.plain(x3), 1, 16, 16, 64)  # 3 channels

@@ -415,15 +415,18 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
 // As[m][BK+4], Bs[n][BK+4] (k contiguous).  In a group of 8 k, MFMA step s takes k-slot 0 =
 // k0+s and k-slot 1 = k0+4+s, so lane (row, half) feeds 4 consecutive MFMAs from ONE
 // ds_read_b128 of its row.  Row stride BK+4 floats makes those reads conflict-free.
-template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI>
+template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC>
 __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
-    constexpr int LR = BK + 4;
+    constexpr int LR = BK + 4;     // A (and k-contiguous B) LDS row stride, floats
+    constexpr int LB = BN + 4;     // k-major B LDS row stride (n-contiguous weights)
     constexpr int KQ = BK / 4;
+    constexpr int NQ = BN / 4;
     constexpr int AQ = BM * KQ / 256;
     constexpr int BQ = BN * KQ / 256;
     constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int BSZ = BKC ? BN * LR : BK * LB;
     __shared__ __attribute__((aligned(16))) float As[2][BM * LR];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LR];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BSZ];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -431,6 +434,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int M_rem = (g.M - m0) < BM ? (int)(g.M - m0) : BM;
+    const int K = g.K;
 
     // A: this thread stages k-quad kq of rows arow + (256/KQ) r
     const int kq = tid % KQ;
@@ -454,16 +458,26 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             aoff[r] = -1;
         }
     }
-    // B: k-contiguous (bkc) -> quads along k of columns; else quads along n of k-rows
-    const bool bkc = g.sbk == 1;
-    constexpr int NQ = BN / 4;
-    const int bkq = tid % KQ, bcol = tid / KQ;     // bkc mapping
-    const int bnq = tid % NQ, bkrow = tid / NQ;    // n-contiguous mapping
+    // B: per-thread element offsets at k0 = 0 (-1: column out of range); k advances by sbk
+    const int sbk = (int)g.sbk, sbn = (int)g.sbn;
+    const int bq_k = BKC ? tid % KQ : tid / NQ;      // k-quad (BKC) or k-row (n-contiguous)
+    const int bq_n = BKC ? tid / KQ : tid % NQ;      // column (BKC) or n-quad
+    int boff[BQ];
+#pragma unroll
+    for (int r = 0; r < BQ; ++r) {
+        if constexpr (BKC) {
+            const int n = n0 + bq_n + (256 / KQ) * r;
+            boff[r] = n < g.N ? n * sbn + 4 * bq_k : -1;
+        } else {
+            const int n = n0 + 4 * bq_n;
+            boff[r] = n < g.N ? (bq_k + (256 / NQ) * r) * sbk + n : -1;
+        }
+    }
 
     float4 ra[AQ], rb[BQ];
     auto load_stage = [&](int k0) {
         const int k = k0 + 4 * kq;
-        const bool kv = k < g.K;
+        const bool kv = k < K;
         int koff = k;
         float4 sc = f4(1.f), sh = f4(0.f);
         if constexpr (AMODE == A_UNSHUFFLE) {
@@ -495,15 +509,8 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         }
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
-            float4 v = f4(0.f);
-            if (bkc) {
-                const int n = n0 + bcol + (256 / KQ) * r, kk = k0 + 4 * bkq;
-                if (n < g.N && kk < g.K) v = ld4(g.B + (int64_t)n * g.sbn + kk);
-            } else {
-                const int kk = k0 + bkrow + (256 / NQ) * r, n = n0 + 4 * bnq;
-                if (n < g.N && kk < g.K) v = ld4(g.B + (int64_t)kk * g.sbk + n);
-            }
-            rb[r] = v;
+            const int kk = BKC ? k0 + 4 * bq_k : k0 + bq_k + (256 / NQ) * r;
+            rb[r] = (boff[r] >= 0 && kk < K) ? ld4(g.B + boff[r] + (BKC ? k0 : k0 * sbk)) : f4(0.f);
         }
     };
     auto store_stage = [&](int buf) {
@@ -512,15 +519,10 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             *reinterpret_cast<float4*>(&As[buf][(arow + (256 / KQ) * r) * LR + 4 * kq]) = ra[r];
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
-            if (bkc) {
-                *reinterpret_cast<float4*>(&Bs[buf][(bcol + (256 / KQ) * r) * LR + 4 * bkq]) = rb[r];
-            } else {
-                const int kk = bkrow + (256 / NQ) * r, nn = 4 * bnq;
-                Bs[buf][(nn + 0) * LR + kk] = rb[r].x;
-                Bs[buf][(nn + 1) * LR + kk] = rb[r].y;
-                Bs[buf][(nn + 2) * LR + kk] = rb[r].z;
-                Bs[buf][(nn + 3) * LR + kk] = rb[r].w;
-            }
+            if constexpr (BKC)
+                *reinterpret_cast<float4*>(&Bs[buf][(bq_n + (256 / KQ) * r) * LR + 4 * bq_k]) = rb[r];
+            else
+                *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = rb[r];
         }
     };
 
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
-    const int nk = (g.K + BK - 1) / BK;
+    const int nk = (K + BK - 1) / BK;
     load_stage(0);
     store_stage(0);
     __syncthreads();
@@ -546,8 +548,15 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             for (int tm = 0; tm < TM; ++tm)
                 af[tm] = *reinterpret_cast<const float4*>(&As[buf][(wm * (BM / 2) + tm * 32 + lo) * LR + kg * 8 + 4 * hi]);
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-                bf[tn] = *reinterpret_cast<const float4*>(&Bs[buf][(wn * (BN / 2) + tn * 32 + lo) * LR + kg * 8 + 4 * hi]);
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * (BN / 2) + tn * 32 + lo;
+                if constexpr (BKC) {
+                    bf[tn] = *reinterpret_cast<const float4*>(&Bs[buf][col * LR + kg * 8 + 4 * hi]);
+                } else {
+                    const float* bp = &Bs[buf][(kg * 8 + 4 * hi) * LB + col];
+                    bf[tn] = make_float4(bp[0], bp[LB], bp[2 * LB], bp[3 * LB]);
+                }
+            }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -804,6 +813,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
 // ------------------------------------------------------------------------------ launchers ----
 bool rows_vec_ok(const RowsArgs& a, int amode) {
     if (a.K % 4 || a.N % 4) return false;
+    if (a.sbk * (int64_t)a.K + a.sbn * (int64_t)a.N >= (int64_t(1) << 31)) return false;
     if (amode == A_UNSHUFFLE && a.uf % 4) return false;
     if (amode != A_UNSHUFFLE && a.a.c0 % 4) return false;
     if (a.sbk != 1 && a.sbn != 1) return false;
@@ -814,12 +824,15 @@ template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     const unsigned gm = (unsigned)cdiv(a.M, 128);
     if (rows_vec_ok(a, AMODE)) {
+        const bool bkc = a.sbk == 1;
         if (a.N <= 64) {
             dim3 grid(gm, (unsigned)cdiv(a.N, 64));
-            gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+            if (bkc) gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
+            else gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
         } else {
             dim3 grid(gm, (unsigned)cdiv(a.N, 128));
-            gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+            if (bkc) gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
+            else gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
         }
         UNET_CHECK_LAUNCH(what);
         return 0;
@@ -844,8 +857,8 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     w.bp = P > 64 ? 128 : 64;
     w.bq = Q > 64 ? 128 : 64;
     w.tiles = (int)(cdiv(P, w.bp) * cdiv(Q, w.bq));
-    int64_t want = cdiv(2048, w.tiles);
-    int64_t maxs = M / 256;
+    int64_t want = cdiv(1024, w.tiles);  // ~4 blocks per CU
+    int64_t maxs = M / 512;               // >= 32 k-steps per block: fewer, cheaper slabs
     if (maxs < 1) maxs = 1;
     int64_t S = want < maxs ? want : maxs;
     if (S < 1) S = 1;

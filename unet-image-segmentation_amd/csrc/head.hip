@@ -22,31 +22,45 @@ namespace {
 constexpr int kMaxCin = 256;
 constexpr int kMaxCls = 32;
 
+// Pixel tile of TP = 8192 / Cin (binary) or 4096 / Cin (multi-class) pixels: the tile's activations are staged through LDS with
+// coalesced float4 loads (one lane per channel quad), then one lane per pixel forms the logits.
 template <int MODE, int NC>
 __global__ __launch_bounds__(256) void head_fwd_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
                                                        const float* __restrict__ bias, float* __restrict__ prob) {
-    const int Cin = v.c0;
-    __shared__ float Ws[kMaxCin * NC];
-    __shared__ float bs[NC];
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int Cin = v.c0, CQ = Cin / 4, LA = Cin + 1, TP = min(256, (NC == 1 ? 8192 : 4096) / Cin);  // LDS <= 64 KB
+    float* Ws = smem;                // [Cin][NC]
+    float* bs = Ws + kMaxCin * NC;   // [NC]
+    float* A = bs + NC;              // [TP][Cin + 1]
     for (int i = threadIdx.x; i < Cin * NC; i += 256) {
         const int k = i / NC, c = i % NC;
         Ws[i] = c < ncls ? W[k * ncls + c] : 0.f;
     }
     if (threadIdx.x < NC) bs[threadIdx.x] = (threadIdx.x < ncls && bias) ? bias[threadIdx.x] : 0.f;
-    __syncthreads();
-    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+    for (int64_t m0 = (int64_t)blockIdx.x * TP; m0 < M; m0 += (int64_t)gridDim.x * TP) {
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < TP * CQ; idx += 256) {
+            const int p = idx / CQ, kq = idx - (idx / CQ) * CQ;
+            const int64_t m = m0 + p;
+            float4 x = f4(0.f);
+            if (m < M) x = row_load4<MODE, false>(v, m, 4 * kq);
+            float* a = A + p * LA + 4 * kq;
+            a[0] = x.x;
+            a[1] = x.y;
+            a[2] = x.z;
+            a[3] = x.w;
+        }
+        __syncthreads();
+        const int p = threadIdx.x;
+        const int64_t m = m0 + p;
+        if (p >= TP || m >= M) continue;
         float l[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) l[c] = bs[c];
-        for (int k = 0; k < Cin; k += 4) {
-            const float4 x = row_load4<MODE, false>(v, m, k);
+        for (int k = 0; k < Cin; ++k) {
+            const float a = A[p * LA + k];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                l[c] = fmaf(x.x, Ws[(k + 0) * NC + c], l[c]);
-                l[c] = fmaf(x.y, Ws[(k + 1) * NC + c], l[c]);
-                l[c] = fmaf(x.z, Ws[(k + 2) * NC + c], l[c]);
-                l[c] = fmaf(x.w, Ws[(k + 3) * NC + c], l[c]);
-            }
+            for (int c = 0; c < NC; ++c) l[c] = fmaf(a, Ws[k * NC + c], l[c]);
         }
         if (ncls == 1) {
             prob[m] = 1.0f / (1.0f + expf(-l[0]));
@@ -155,7 +169,77 @@ __global__ __launch_bounds__(256) void dice_finalize_kernel(const float* __restr
     }
 }
 
-// dlogit and dx for one pixel per lane
+// d(loss)/d(prob) for one (pixel, class) from the per-(image, class) sums
+template <int LOSS>
+__device__ __forceinline__ float loss_grad(float t, const float* s3, float smooth, float gscale) {
+    const float I = s3[0], T = s3[1], P = s3[2];
+    if constexpr (LOSS == UNET_LOSS_DICE) {
+        const float nm = 2.0f * I + smooth, den = T + P + smooth;
+        return -gscale * (2.0f * t * den - nm) / (den * den);
+    } else {
+        const float j = I + smooth, u = T + P - I + smooth;
+        return -gscale * (t * u - j * (1.0f - t)) / (u * u);
+    }
+}
+
+// Binary head (ncls == 1), fully fused backward over 256-pixel tiles:
+//   phase 1: one lane per pixel -> dlogit = dL/dp * p (1 - p) into LDS (and the db sum);
+//   phase 2: one lane per (pixel, channel quad), coalesced: dx = W dlogit, and
+//            dW += relu(bn(z)) * dlogit accumulated in registers across tiles;
+//   end: fixed-order LDS reduction -> per-block partials of dW (Cin) and db (1).
+template <int MODE, int LOSS>
+__global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int64_t hw, const float* __restrict__ W,
+                                                        const float* __restrict__ prob, const float* __restrict__ yt,
+                                                        const float* __restrict__ sums, float smooth, float gscale,
+                                                        float* __restrict__ dx, float* __restrict__ part_w,
+                                                        float* __restrict__ part_b) {
+    __shared__ float dls[256];
+    __shared__ float4 red[256];
+    const int Cin = v.c0, CQ = Cin / 4;
+    const int kq = threadIdx.x % CQ;  // CQ divides 256 (launcher checks)
+    const float4 w4 = ld4(W + 4 * kq);
+    float4 dw = f4(0.f);
+    float db = 0.f;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        __syncthreads();
+        {
+            const int64_t m = m0 + threadIdx.x;
+            float dl = 0.f;
+            if (m < M) {
+                const float p = prob[m];
+                const float g = loss_grad<LOSS>(yt[m], sums + (m / hw) * 3, smooth, gscale);
+                dl = g * p * (1.0f - p);
+            }
+            dls[threadIdx.x] = dl;
+            db += dl;
+        }
+        __syncthreads();
+        for (int p = threadIdx.x / CQ; p < 256; p += 256 / CQ) {
+            const int64_t m = m0 + p;
+            if (m >= M) break;
+            const float dl = dls[p];
+            const float4 a = row_load4<MODE, false>(v, m, 4 * kq);
+            dw = fma4(a, f4(dl), dw);
+            st4(dx + m * Cin + 4 * kq, mul4(w4, f4(dl)));
+        }
+    }
+    __syncthreads();
+    red[threadIdx.x] = dw;
+    __syncthreads();
+    if (threadIdx.x < CQ) {
+        float4 s = red[threadIdx.x];
+        for (int q = threadIdx.x + CQ; q < 256; q += CQ) s = add4(s, red[q]);
+        st4(part_w + (int64_t)blockIdx.x * Cin + 4 * threadIdx.x, s);
+    }
+    const float dbs = wave_sum(db);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) dls[threadIdx.x >> 6] = dbs;
+    __syncthreads();
+    if (threadIdx.x == 0) part_b[blockIdx.x] = dls[0] + dls[1] + dls[2] + dls[3];
+}
+
+// Multi-class head: dlogit (softmax backward) to global for the weight-gradient GEMM, and dx
+// written coalesced per (pixel, channel quad) from LDS copies of W and the tile's dlogits.
 template <int NC, int LOSS>
 __global__ __launch_bounds__(256) void head_bwd_kernel(int64_t M, int64_t hw, int Cin, int ncls,
                                                        const float* __restrict__ W, const float* __restrict__ prob,
@@ -163,56 +247,51 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(int64_t M, int64_t hw, in
                                                        float smooth, float gscale, float* __restrict__ dlogit,
                                                        float* __restrict__ dx) {
     __shared__ float Ws[kMaxCin * NC];
+    __shared__ float dls[256 * NC];
     for (int i = threadIdx.x; i < Cin * NC; i += 256) {
         const int k = i / NC, c = i % NC;
         Ws[i] = c < ncls ? W[k * ncls + c] : 0.f;
     }
-    __syncthreads();
-    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
-        const int n = (int)(m / hw);
-        float p[NC], dl[NC];
+    const int CQ = Cin / 4;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        __syncthreads();
+        {
+            const int64_t m = m0 + threadIdx.x;
+            float p[NC], dl[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            p[c] = 0.f;
-            dl[c] = 0.f;
-            if (c < ncls) {
-                const float pc = prob[m * ncls + c], t = yt[m * ncls + c];
-                const float* s3 = sums + ((int64_t)n * ncls + c) * 3;
-                const float I = s3[0], T = s3[1], P = s3[2];
-                float dp;
-                if constexpr (LOSS == UNET_LOSS_DICE) {
-                    const float nm = 2.0f * I + smooth, den = T + P + smooth;
-                    dp = -gscale * (2.0f * t * den - nm) / (den * den);
-                } else {
-                    const float j = I + smooth, u = T + P - I + smooth;
-                    dp = -gscale * (t * u - j * (1.0f - t)) / (u * u);
+            for (int c = 0; c < NC; ++c) {
+                p[c] = 0.f;
+                dl[c] = 0.f;
+                if (c < ncls && m < M) {
+                    p[c] = prob[m * ncls + c];
+                    dl[c] = loss_grad<LOSS>(yt[m * ncls + c], sums + ((m / hw) * ncls + c) * 3, smooth, gscale);
                 }
-                p[c] = pc;
-                dl[c] = dp;
             }
-        }
-        if (ncls == 1) {
-            dl[0] = dl[0] * p[0] * (1.0f - p[0]);
-        } else {
             float s = 0.f;
 #pragma unroll
             for (int c = 0; c < NC; ++c) s = fmaf(dl[c], p[c], s);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) dl[c] = p[c] * (dl[c] - s);
+            for (int c = 0; c < NC; ++c) {
+                dl[c] = p[c] * (dl[c] - s);
+                dls[threadIdx.x * NC + c] = dl[c];
+                if (c < ncls && m < M) dlogit[m * ncls + c] = dl[c];
+            }
         }
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-            if (c < ncls) dlogit[m * ncls + c] = dl[c];
-        for (int k = 0; k < Cin; k += 4) {
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < 256 * CQ; idx += 256) {
+            const int p = idx / CQ, kq = idx - (idx / CQ) * CQ;
+            const int64_t m = m0 + p;
+            if (m >= M) continue;
             float4 o = f4(0.f);
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                o.x = fmaf(Ws[(k + 0) * NC + c], dl[c], o.x);
-                o.y = fmaf(Ws[(k + 1) * NC + c], dl[c], o.y);
-                o.z = fmaf(Ws[(k + 2) * NC + c], dl[c], o.z);
-                o.w = fmaf(Ws[(k + 3) * NC + c], dl[c], o.w);
+                const float d = dls[p * NC + c];
+                o.x = fmaf(Ws[(4 * kq + 0) * NC + c], d, o.x);
+                o.y = fmaf(Ws[(4 * kq + 1) * NC + c], d, o.y);
+                o.z = fmaf(Ws[(4 * kq + 2) * NC + c], d, o.z);
+                o.w = fmaf(Ws[(4 * kq + 3) * NC + c], d, o.w);
             }
-            st4(dx + m * Cin + k, o);
+            st4(dx + m * Cin + 4 * kq, o);
         }
     }
 }
@@ -305,17 +384,22 @@ extern "C" int unet_head_fwd(const unet_view* x, int n, int h, int w, int ncls, 
     const DView v = make_dview(*x);
     const int64_t M = (int64_t)n * h * w;
     hipStream_t st = as_stream(stream);
-    const int grid = grid_for(M);
+    const int TP = (ncls > 1 ? 4096 : 8192) / x->c0 < 256 ? (ncls > 1 ? 4096 : 8192) / x->c0 : 256;
+    int64_t g = cdiv(M, TP);
+    const int grid = (int)(g > 4096 ? 4096 : g);
+    const bool multi = ncls > 1;
+    const size_t smem = ((size_t)kMaxCin * (multi ? kMaxCls : 1) + (multi ? kMaxCls : 1) +
+                         (size_t)TP * (x->c0 + 1)) * sizeof(float);
     if (x->mode == UNET_VIEW_BNRELU) {
-        if (ncls == 1)
-            head_fwd_kernel<UNET_VIEW_BNRELU, 1><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+        if (!multi)
+            head_fwd_kernel<UNET_VIEW_BNRELU, 1><<<grid, 256, smem, st>>>(v, M, ncls, kernel, bias, prob);
         else
-            head_fwd_kernel<UNET_VIEW_BNRELU, kMaxCls><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+            head_fwd_kernel<UNET_VIEW_BNRELU, kMaxCls><<<grid, 256, smem, st>>>(v, M, ncls, kernel, bias, prob);
     } else {
-        if (ncls == 1)
-            head_fwd_kernel<UNET_VIEW_PLAIN, 1><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+        if (!multi)
+            head_fwd_kernel<UNET_VIEW_PLAIN, 1><<<grid, 256, smem, st>>>(v, M, ncls, kernel, bias, prob);
         else
-            head_fwd_kernel<UNET_VIEW_PLAIN, kMaxCls><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob);
+            head_fwd_kernel<UNET_VIEW_PLAIN, kMaxCls><<<grid, 256, smem, st>>>(v, M, ncls, kernel, bias, prob);
     }
     UNET_CHECK_LAUNCH("unet_head_fwd");
     return 0;
@@ -353,7 +437,9 @@ extern "C" size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
     size_t a = head_wgrad_workspace(M, cin, ncls);
     size_t b = colsum_workspace(M, ncls);
-    return dl + (a > b ? a : b);
+    const size_t fused = align_up((size_t)1024 * cin, 64) * sizeof(float) + 1024 * sizeof(float);
+    const size_t gen = dl + (a > b ? a : b);
+    return align_up(fused > gen ? fused : gen, 256);
 }
 
 extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
@@ -372,12 +458,36 @@ extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, 
     const int64_t M = (int64_t)n * h * w;
     const int64_t hw = (int64_t)h * w;
     hipStream_t st = as_stream(stream);
+    const float gscale = 1.0f / (float)((int64_t)n * ncls);
+    const DView v = make_dview(*x);
+    const int CQ = x->c0 / 4;
+    if (ncls == 1 && 256 % CQ == 0) {
+        int64_t g = cdiv(M, 256);
+        const int grid = (int)(g > 1024 ? 1024 : g);
+        float* part_w = static_cast<float*>(ws);
+        float* part_b = part_w + align_up((size_t)grid * x->c0, 64);
+#define UNET_HB1(MODE, L)                                                                                     \
+    head_bwd1_kernel<MODE, L><<<grid, 256, 0, st>>>(v, M, hw, kernel, prob, y_true, sums, smooth, gscale, dx, \
+                                                     part_w, part_b)
+        if (x->mode == UNET_VIEW_BNRELU) {
+            if (loss_kind == UNET_LOSS_DICE) UNET_HB1(UNET_VIEW_BNRELU, UNET_LOSS_DICE);
+            else UNET_HB1(UNET_VIEW_BNRELU, UNET_LOSS_IOU);
+        } else {
+            if (loss_kind == UNET_LOSS_DICE) UNET_HB1(UNET_VIEW_PLAIN, UNET_LOSS_DICE);
+            else UNET_HB1(UNET_VIEW_PLAIN, UNET_LOSS_IOU);
+        }
+#undef UNET_HB1
+        UNET_CHECK_LAUNCH("unet_head_bwd");
+        int rc = reduce_slabs(part_w, grid, x->c0, dkernel, x->c0, x->c0, st);
+        if (rc) return rc;
+        return reduce_slabs(part_b, grid, 1, dbias, 1, 1, st);
+    }
     float* dlogit = static_cast<float*>(ws);
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
     void* ws2 = static_cast<char*>(ws) + dl;
     const size_t ws2_bytes = ws_bytes - dl;
-    const float gscale = 1.0f / (float)((int64_t)n * ncls);
-    const int grid = grid_for(M);
+    int64_t g = cdiv(M, 256);
+    const int grid = (int)(g > 4096 ? 4096 : g);
 #define UNET_HB(NC, L)                                                                                        \
     head_bwd_kernel<NC, L><<<grid, 256, 0, st>>>(M, hw, x->c0, ncls, kernel, prob, y_true, sums, smooth, gscale, \
                                                  dlogit, dx)

@@ -9,36 +9,98 @@ namespace unet {
 namespace {
 thread_local char g_err[512] = "";
 
-// out[l] = sum_s part[s][l], s in a fixed order.  Block = 64 columns x G s-groups;
-// each thread sums s = g, g+G, ... in double, then group 0 adds the G partials in order.
-__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L,
-                                                            float* __restrict__ out, int64_t row, int64_t ld_out) {
-    const int G = blockDim.x / 64;
-    const int lane = threadIdx.x & 63;
-    const int g = threadIdx.x >> 6;
-    const int64_t l = (int64_t)blockIdx.x * 64 + lane;
-    double acc = 0.0;
+__device__ __forceinline__ void store_out(float* out, int64_t l, int64_t row, int64_t ld_out, double v) {
+    out[(l / row) * ld_out + (l % row)] = (float)v;
+}
+
+// out[l] = sum_s part[s][l] with s in increasing order, in double.  Wide reductions (many
+// outputs): one thread per 4 consecutive outputs walks all S slabs with float4 loads.
+__global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restrict__ part, int S, int64_t L,
+                                                           float* __restrict__ out, int64_t row, int64_t ld_out) {
+    const int64_t l = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (l >= L) return;
+    const float* p = part + l;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld4(p + (int64_t)(s + u) * L);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a0 += (double)v[u].x;
+            a1 += (double)v[u].y;
+            a2 += (double)v[u].z;
+            a3 += (double)v[u].w;
+        }
+    }
+    for (; s < S; ++s) {
+        const float4 v = ld4(p + (int64_t)s * L);
+        a0 += (double)v.x;
+        a1 += (double)v.y;
+        a2 += (double)v.z;
+        a3 += (double)v.w;
+    }
+    store_out(out, l, row, ld_out, a0);
+    store_out(out, l + 1, row, ld_out, a1);
+    store_out(out, l + 2, row, ld_out, a2);
+    store_out(out, l + 3, row, ld_out, a3);
+}
+
+// Tall reductions (few outputs, many slabs): block = 16 output quads x 32 slab groups; group g
+// sums s = g, g+32, ... and a fixed-order tree adds the 32 group partials.
+__global__ __launch_bounds__(512) void reduce_tall4_kernel(const float* __restrict__ part, int S, int64_t L,
+                                                           float* __restrict__ out, int64_t row, int64_t ld_out) {
+    constexpr int LQ = 16, G = 32;
+    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
+    const int64_t l = ((int64_t)blockIdx.x * LQ + q) * 4;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (l < L) {
         int s = g;
-        for (; s + 3 * G < S; s += 4 * G) {
-            float a0 = part[(int64_t)s * L + l];
-            float a1 = part[(int64_t)(s + G) * L + l];
-            float a2 = part[(int64_t)(s + 2 * G) * L + l];
-            float a3 = part[(int64_t)(s + 3 * G) * L + l];
-            acc += (double)a0;
-            acc += (double)a1;
-            acc += (double)a2;
-            acc += (double)a3;
+        for (; s + G < S; s += 2 * G) {
+            const float4 v0 = ld4(part + (int64_t)s * L + l);
+            const float4 v1 = ld4(part + (int64_t)(s + G) * L + l);
+            a[0] += (double)v0.x; a[1] += (double)v0.y; a[2] += (double)v0.z; a[3] += (double)v0.w;
+            a[0] += (double)v1.x; a[1] += (double)v1.y; a[2] += (double)v1.z; a[3] += (double)v1.w;
         }
-        for (; s < S; s += G) acc += (double)part[(int64_t)s * L + l];
+        if (s < S) {
+            const float4 v0 = ld4(part + (int64_t)s * L + l);
+            a[0] += (double)v0.x; a[1] += (double)v0.y; a[2] += (double)v0.z; a[3] += (double)v0.w;
+        }
     }
-    __shared__ double red[16][64];
+    __shared__ double red[4][G * LQ];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+    __syncthreads();
+    for (int half = G / 2; half > 0; half >>= 1) {
+        if (g < half) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + half * LQ];
+        }
+        __syncthreads();
+    }
+    if (g == 0 && l < L) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) store_out(out, l + k, row, ld_out, red[k][q]);
+    }
+}
+
+// Scalar fallback for L % 4 != 0: block = 64 outputs x 16 slab groups.
+__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L,
+                                                            float* __restrict__ out, int64_t row, int64_t ld_out) {
+    constexpr int G = 16;
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t l = (int64_t)blockIdx.x * 64 + lane;
+    double acc = 0.0;
+    if (l < L)
+        for (int s = g; s < S; s += G) acc += (double)part[(int64_t)s * L + l];
+    __shared__ double red[G][64];
     red[g][lane] = acc;
     __syncthreads();
     if (g == 0 && l < L) {
         double t = red[0][lane];
         for (int k = 1; k < G; ++k) t += red[k][lane];
-        out[(l / row) * ld_out + (l % row)] = (float)t;
+        store_out(out, l, row, ld_out, t);
     }
 }
 }  // namespace
@@ -71,9 +133,14 @@ int check_view(const unet_view* v, const char* op, bool need_vec4) {
 
 int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream) {
     UNET_CHECK_ARG(S >= 1 && L >= 1 && row >= 1, "reduce_slabs: bad sizes");
-    int G = S < 16 ? S : 16;
-    dim3 grid((unsigned)cdiv(L, 64));
-    reduce_slabs_kernel<<<grid, 64 * G, 0, stream>>>(part, S, L, out, row, ld_out);
+    const bool vec = L % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
+    if (vec && (cdiv(L, 1024) >= 64 || S <= 32)) {
+        reduce_cols4_kernel<<<(unsigned)cdiv(L, 1024), 256, 0, stream>>>(part, S, L, out, row, ld_out);
+    } else if (vec) {
+        reduce_tall4_kernel<<<(unsigned)cdiv(L, 64), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+    } else {
+        reduce_slabs_kernel<<<(unsigned)cdiv(L, 64), 1024, 0, stream>>>(part, S, L, out, row, ld_out);
+    }
     UNET_CHECK_LAUNCH("reduce_slabs");
     return 0;
 }

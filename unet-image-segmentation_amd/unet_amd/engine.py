@@ -16,6 +16,7 @@ Data layout in HBM (per GPU, batch N):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence
 
@@ -64,6 +65,8 @@ class BlockBufs:
     scale: torch.Tensor
     shift: torch.Tensor
     da: torch.Tensor  # gradient w.r.t. this block's output activation
+    dz: Optional[torch.Tensor] = None  # backward-only, allocated on first backward
+    dy: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -120,6 +123,13 @@ class UNetEngine:
         self._acts: Dict[int, Acts] = {}
         self.step_count = 0
         self.grad_hook: Optional[Callable[[int], None]] = None  # called with a flat-offset low-water mark
+        # Off-critical-path backward work (weight gradients of the pointwise and depthwise
+        # convolutions) runs on a second HIP stream, overlapping the data-gradient chain.
+        self.side = torch.cuda.Stream(device=self.device)
+        self.overlap = os.environ.get("UNET_OVERLAP", "1") != "0"  # 0: single stream (clean profiles)
+        # fused depthwise+pointwise forward: used where it measured faster than the two launches
+        # (tools/bench_sepconv.py: inference at >= 128x128; training keeps y, so the split path wins)
+        self.fuse_sepconv = "infer"
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -211,8 +221,22 @@ class UNetEngine:
         h, w = self._dims(b.level)
         m = n * h * w
         bb = A.blocks[b.name]
-        ops.dwconv3x3_fwd(view, n, h, w, self.vars[f"{b.name}_sepconv/depthwise_kernel"], bb.y)
         gamma, beta, mm, mv = self._bn(b.name)
+        dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
+        pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
+        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "infer" and not training and h * w >= 128 * 128)
+        if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
+            # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight grad
+            stats = training and self.use_bn
+            ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if training else None, bb.z,
+                            bb.part if stats else None)
+            if stats:
+                ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean,
+                                bb.rstd, bb.scale, bb.shift)
+            else:
+                ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
+            return View.bnrelu(bb.z, bb.scale, bb.shift)
+        ops.dwconv3x3_fwd(view, n, h, w, dk, bb.y)
         if training and self.use_bn:
             ops.pointwise_fwd(bb.y, m, b.cin, b.cout, self.vars[f"{b.name}_sepconv/pointwise_kernel"], bb.z, bb.part)
             ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
@@ -269,16 +293,26 @@ class UNetEngine:
 
     # ----------------------------------------------------------------- backward ------
     def _grads_ready(self, name: str):
+        """Gradients at flat offsets >= offset(name) are final once both streams get here:
+        the hook (bucketed all-reduce) is issued from the side stream after it has caught up
+        with the main stream."""
         if self.grad_hook is not None:
-            self.grad_hook(self.train_layout.offsets[name])
+            if self.overlap:
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    self.grad_hook(self.train_layout.offsets[name])
+            else:
+                self.grad_hook(self.train_layout.offsets[name])
 
     def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0):
         n = A.n
         h, w = self._dims(b.level)
         m = n * h * w
         bb = A.blocks[b.name]
-        dz = A.dz[:m * b.cout]
-        dy = A.dy[:m * b.cin]
+        if bb.dz is None:
+            bb.dz = torch.empty(m * b.cout, dtype=torch.float32, device=self.device)
+            bb.dy = torch.empty(m * b.cin, dtype=torch.float32, device=self.device)
+        dz, dy = bb.dz, bb.dy
         if self.use_bn:
             dgamma, dbeta = self.gvars[f"{b.name}_bn/gamma"], self.gvars[f"{b.name}_bn/beta"]
         else:
@@ -287,9 +321,17 @@ class UNetEngine:
                         drop_seed, dgamma, dbeta, dz)
         pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
         dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
-        ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, self.gvars[f"{b.name}_sepconv/pointwise_kernel"])
         ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
-        ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, self.gvars[f"{b.name}_sepconv/depthwise_kernel"])
+        gpk = self.gvars[f"{b.name}_sepconv/pointwise_kernel"]
+        gdk = self.gvars[f"{b.name}_sepconv/depthwise_kernel"]
+        if self.overlap:  # weight gradients off the critical path, on the side stream
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
+                ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+        else:
+            ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
+            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
         if dx0 is not None:
             ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
@@ -344,6 +386,8 @@ class UNetEngine:
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
+        if self.overlap:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
 
     # --------------------------------------------------------------- train step ------
     def forward_train(self, x: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:

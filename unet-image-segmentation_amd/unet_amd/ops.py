@@ -233,6 +233,28 @@ def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
           _ptr(dz), m, cin, cout, _ptr(dpk), ws, wsb, _stream())
 
 
+def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
+    vs = x.c_struct()
+    return bool(L.load().unet_sepconv_fwd_supported(ctypes.byref(vs), n, h, w, cout))
+
+
+def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tensor, y: Optional[Tensor],
+                z: Tensor, partials: Optional[Tensor] = None):
+    """Fused depthwise 3x3 + pointwise 1x1 (+ BN partials); y (depthwise output) optional."""
+    C = x.channels
+    m = n * h * w
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(pk, "pointwise_kernel", C * cout)
+    _check(z, "z", m * cout)
+    if y is not None:
+        _check(y, "y", m * C)
+    if partials is not None:
+        _check(partials, "bn_partials", bn_partials_numel(m, cout))
+    vs = x.c_struct()
+    _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C, 4.0 * (m * C + m * cout + C * cout)),
+          ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _stream())
+
+
 # ------------------------------------------------------------------ BatchNorm ---
 def bn_finalize(partials: Tensor, m: int, c: int, gamma, beta, eps, momentum, moving_mean, moving_var,
                 update_moving: bool, mean, rstd, scale, shift):
