@@ -31,6 +31,20 @@ PEAK_HBM_GBS = 8000.0
 ROOFLINE_OP = "unet_pointwise_fwd"
 
 
+def pmc_traffic(op):
+    """HBM bytes per launch of `op` from the newest committed PMC summary (profiles/*_traffic.json,
+    written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("op") == op:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def synthetic_batch(n, h, w, ncls, seed, device):
     import numpy as np
     import torch
@@ -157,9 +171,12 @@ def main():
             if s:
                 avg_ms = s["ms"] / s["launches"]
                 ach = s["flops"] / (s["ms"] * 1e-3) / 1e12
+                traffic, tsrc = pmc_traffic(ROOFLINE_OP)
                 out["roofline"] = {"bound": "mfma", "kernel": ROOFLINE_OP, "achieved": round(ach, 2),
                                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                                   "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                                   "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                                   "traffic_source": tsrc,
+                                   "algorithmic_bytes_per_launch": round(s["bytes"] / s["launches"]),
                                    "launches_per_step": s["launches"] // args.steps,
                                    "avg_launch_us": round(avg_ms * 1e3, 2),
                                    "algorithmic_gflop_per_step": round(s["flops"] / args.steps / 1e9, 3)}

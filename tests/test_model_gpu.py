@@ -105,14 +105,21 @@ def test_builder_api_and_inference_parity_cfg1():
     assert np.abs(prob_split - ref).max() < 2e-5 and np.abs(prob_fused - ref).max() < 2e-5
 
 
-@pytest.mark.parametrize("ncls,use_bn,drop,loss", [(1, True, 0.0, "dice_loss"), (1, True, 0.2, "dice_loss"),
-                                                   (21, True, 0.0, "dice_loss"), (1, False, 0.0, "dice_loss"),
-                                                   (1, True, 0.0, "iou_loss")])
-def test_train_step_parity(ncls, use_bn, drop, loss):
+@pytest.mark.parametrize("ncls,use_bn,drop,loss,fuse", [(1, True, 0.0, "dice_loss", "never"),
+                                                        (1, True, 0.2, "dice_loss", "never"),
+                                                        (21, True, 0.0, "dice_loss", "auto"),
+                                                        (1, False, 0.0, "dice_loss", "auto"),
+                                                        (1, True, 0.0, "iou_loss", "auto"),
+                                                        (1, True, 0.0, "dice_loss", "always"),
+                                                        (1, True, 0.2, "dice_loss", "always")])
+def test_train_step_parity(ncls, use_bn, drop, loss, fuse):
+    """One train step against the oracle; fuse="always" runs the fused depthwise+pointwise
+    forward on every level it supports (32x32 and 16x16 here), "never" the split kernels."""
     from unet_amd.model import UNetModel
     from unet_amd.optim import AdamW
     n, hw = 2, 32
     model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
+    model.engine.fuse_sepconv = fuse
     orc = UNetOracle(ncls, drop, use_bn)
     lr, wd = 2e-3, 1e-4
     okind = "dice" if loss == "dice_loss" else "iou"

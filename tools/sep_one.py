@@ -1,0 +1,28 @@
+"""Run the fused sepconv forward (or the split dw + pw pair) on one shape repeatedly, for
+rocprofv3 --pmc passes.  usage: sep_one.py MODE H W CIN COUT [iters] [split]"""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "unet-image-segmentation_amd"), ROOT]
+import torch
+from unet_amd import ops
+mode, h, w, C, cout = (int(v) for v in sys.argv[1:6])
+iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+split = len(sys.argv) > 7 and sys.argv[7] == "split"
+N = 16
+big = 2 if mode == 2 else 1
+src = torch.randn(N, big * h, big * w, C, device="cuda")
+sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+v = ops.View.plain(src) if mode == 0 else (ops.View.pool_bnrelu(src, sc, sh) if mode == 2 else ops.View.bnrelu(src, sc, sh))
+m = N * h * w
+dk = torch.randn(3, 3, C, 1, device="cuda")
+pk = torch.randn(1, 1, C, cout, device="cuda") * 0.05
+y = torch.empty(N, h, w, C, device="cuda")
+z = torch.empty(N, h, w, cout, device="cuda")
+part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+for _ in range(iters):
+    if split:
+        ops.dwconv3x3_fwd(v, N, h, w, dk, y)
+        ops.pointwise_fwd(y, m, C, cout, pk, z, part)
+    else:
+        ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part)
+torch.cuda.synchronize()

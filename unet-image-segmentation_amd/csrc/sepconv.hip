@@ -33,20 +33,31 @@ struct SepArgs {
     float2* stats;    // [M/128][Cout]
 };
 
-template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y>
-__global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
+// WN = waves along N (2 or 4); the block has 2 x WN waves, each owning a 64 x (BN / WN) piece of
+// the 128 x BN output tile.  Wide tiles (BN = 256, 8 waves) give two waves per SIMD, so one wave's
+// halo / depthwise work overlaps the other's MFMAs.
+template <int MODE, bool DROP, int EPI, int BN, int WN, bool WRITE_Y>
+__global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g) {
+    constexpr int NT = 128 * WN;              // threads
     constexpr int LB = BN + 4;
-    constexpr int TN = BN / 64;
+    constexpr int TN = BN / (32 * WN);        // 32-column MFMA tiles per wave
     constexpr int NQ = BN / 4;
-    constexpr int BQ = BN * (BK / 4) / 256;  // B float4 per thread per stage
+    constexpr int BQ = BN * (BK / 4) / NT;    // B float4 per thread per stage
     constexpr int NH = HHp * HWp * (BK / 4);  // halo float4 per stage (720)
-    constexpr int HR = (NH + 255) / 256;      // per thread (3)
-    __shared__ __attribute__((aligned(16))) float Xs[HHp * HWp * LR];
+    constexpr int HR = (NH + NT - 1) / NT;    // per thread
+    constexpr int RPT = 512 / NT;             // depthwise output rows per thread (2 or 1)
+    static_assert(TN >= 1 && BQ >= 1, "tile shape");
+    constexpr int XS = HHp * HWp * LR;        // floats per halo buffer
+    // Pipeline (one barrier per k-stage): while the MFMAs consume A/B of stage kt, the same
+    // waves evaluate the depthwise taps of stage kt+1 (halo already in LDS) and the global
+    // loads of halo kt+2 / B kt+1 are in flight.
+    __shared__ __attribute__((aligned(16))) float Xs[2][XS];
+    __shared__ __attribute__((aligned(16))) float Ks[2][9 * BK];
     __shared__ __attribute__((aligned(16))) float As[2][128 * LR];
     __shared__ __attribute__((aligned(16))) float Bs[2][BK * LB];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const int lo = lane & 31, hi = lane >> 5;
     const int tiles_w = g.W / TW, tiles_h = g.H / TH;
     int t = blockIdx.x;
@@ -58,76 +69,150 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
     const int n0 = blockIdx.y * BN;
     const int Cin = g.Cin, C = g.x.C;
 
-    // halo staging geometry: element e = tid + 256 j -> (pixel, quad)
-    float4 rh[HR];
     float4 rb[BQ];
-    float4 rk[9];
-    const int dq = tid & 3;                   // dw_stage: channel quad
-    const int dc = (tid >> 2) & 15, dr = 2 * (tid >> 6);  // dw_stage: pixel column, first of 2 rows
+    float4 rt;
     const int bq_k = tid / NQ, bq_n = tid % NQ;  // n-contiguous B: k-row, n-quad
-    auto load_stage = [&](int k0) {
+    // Halo geometry is fixed per thread across k-stages: element e = tid + 256 j is pixel e/4 of
+    // the 10x18 halo and channel quad e%4 = tid%4 of the stage.  lp = logical pixel index (-1 if
+    // outside the image or past the halo), sp = first source pixel (the 2x2 window for POOL).
+    // Loads are issued unconditionally from clamped addresses and masked / transformed only when
+    // the registers are written to LDS, so no load is waited for before the MFMAs of the stage.
+    constexpr int NP = MODE == UNET_VIEW_POOL_BNRELU ? 4 : 1;  // raw loads per halo element
+    const int hq = tid & 3;
+    int lp[HR], sp[HR];
+#pragma unroll
+    for (int j = 0; j < HR; ++j) {
+        const int e = tid + NT * j;
+        const int pix = e >> 2, r = pix / HWp, cc = pix - r * HWp;
+        const int hh = h0 - 1 + r, ww = w0 - 1 + cc;
+        const bool ok = e < NH && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+        lp[j] = ok ? (n * g.H + hh) * g.W + ww : -1;
+        if constexpr (MODE == UNET_VIEW_POOL_BNRELU)
+            sp[j] = ok ? (n * 2 * g.H + 2 * hh) * (2 * g.W) + 2 * ww : 0;
+        else
+            sp[j] = ok ? lp[j] : 0;
+    }
+    float4 rx[HR][NP];   // raw halo values in flight
+    float4 rsc, rsh;     // BN affine of this thread's channel quad
+    int hc = 0;          // channel of this thread's quad for the staged k0
+    bool hbn = false;
+    auto load_halo = [&](int k0) {
+        const int c = k0 + 4 * hq;
+        hc = c;
+        const bool cok = c < Cin;
+        const float* src = g.x.src0;
+        int cs = g.x.c0, ci = cok ? c : 0;
+        const float* scp = g.x.sc0;
+        const float* shp = g.x.sh0;
+        hbn = MODE == UNET_VIEW_BNRELU || MODE == UNET_VIEW_POOL_BNRELU;
+        if constexpr (MODE == UNET_VIEW_CONCAT) {
+            if (ci >= g.x.c0) {
+                src = g.x.src1;
+                cs = g.x.c1;
+                ci -= g.x.c0;
+                scp = g.x.sc1;
+                shp = g.x.sh1;
+                hbn = true;
+            }
+        }
+        if constexpr (MODE != UNET_VIEW_PLAIN) {
+            rsc = hbn ? ld4(scp + ci) : f4(1.f);
+            rsh = hbn ? ld4(shp + ci) : f4(0.f);
+        }
 #pragma unroll
         for (int j = 0; j < HR; ++j) {
-            const int e = tid + 256 * j;
-            float4 v = f4(0.f);
-            if (e < NH) {
-                const int q = e & 3, pix = e >> 2;
-                const int r = pix / HWp, cc = pix - (pix / HWp) * HWp;
-                const int hh = h0 - 1 + r, ww = w0 - 1 + cc;
-                const int c = k0 + 4 * q;
-                if (hh >= 0 && hh < g.H && ww >= 0 && ww < g.W && c < Cin) {
-                    v = view_load4<MODE>(g.x, n, hh, ww, g.H, g.W, c);
-                    if constexpr (DROP) {
-                        const uint64_t i = ((uint64_t)((n * g.H + hh) * g.W + ww)) * C + c;
-                        v.x *= drop_mult(g.x.seed, i + 0, g.x.rate, g.x.inv_keep);
-                        v.y *= drop_mult(g.x.seed, i + 1, g.x.rate, g.x.inv_keep);
-                        v.z *= drop_mult(g.x.seed, i + 2, g.x.rate, g.x.inv_keep);
-                        v.w *= drop_mult(g.x.seed, i + 3, g.x.rate, g.x.inv_keep);
-                    }
-                }
+            const float* b = src + (sp[j] * cs + ci);
+            rx[j][0] = ld4(b);
+            if constexpr (NP == 4) {
+                const int rs = 2 * g.W * cs;
+                rx[j][1] = ld4(b + cs);
+                rx[j][2] = ld4(b + rs);
+                rx[j][3] = ld4(b + rs + cs);
             }
-            rh[j] = v;
         }
+        // depthwise taps of the stage: 9 x BK floats = 36 float4, tap-major
+        const int tq = tid < 9 * (BK / 4) ? tid : 0;
+        const int tp = tq / (BK / 4), c2 = k0 + 4 * (tq % (BK / 4));
+        rt = ld4(g.dk + tp * Cin + (c2 < Cin ? c2 : 0));
+    };
+    auto store_halo = [&](int buf) {
+        const bool cok = hc < Cin;
+#pragma unroll
+        for (int j = 0; j < HR; ++j) {
+            const int e = tid + NT * j;
+            float4 v = rx[j][0];
+            if constexpr (NP == 4) {
+                v = fma4(v, rsc, rsh);
+                v = max4(v, fma4(rx[j][1], rsc, rsh));
+                v = max4(v, fma4(rx[j][2], rsc, rsh));
+                v = max4(v, fma4(rx[j][3], rsc, rsh));
+                v = relu4(v);
+            } else if constexpr (MODE != UNET_VIEW_PLAIN) {
+                if (hbn) v = bnrelu4(v, rsc, rsh);
+            }
+            if constexpr (DROP) {
+                const uint64_t i = (uint64_t)(lp[j] < 0 ? 0 : lp[j]) * C + hc;
+                v.x *= drop_mult(g.x.seed, i + 0, g.x.rate, g.x.inv_keep);
+                v.y *= drop_mult(g.x.seed, i + 1, g.x.rate, g.x.inv_keep);
+                v.z *= drop_mult(g.x.seed, i + 2, g.x.rate, g.x.inv_keep);
+                v.w *= drop_mult(g.x.seed, i + 3, g.x.rate, g.x.inv_keep);
+            }
+            if (lp[j] < 0 || !cok) v = f4(0.f);
+            if (e < NH) *reinterpret_cast<float4*>(&Xs[buf][(e >> 2) * LR + 4 * (e & 3)]) = v;
+        }
+        if (tid < 9 * (BK / 4)) {
+            const int c2 = hc - 4 * hq + 4 * (tid % (BK / 4));  // k0 + quad of this tap slot
+            *reinterpret_cast<float4*>(&Ks[buf][4 * tid]) = c2 < Cin ? rt : f4(0.f);
+        }
+    };
+    bool bok[BQ];
+    auto load_b = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
-            const int kk = k0 + bq_k + (256 / NQ) * r, nn = n0 + 4 * bq_n;
-            rb[r] = (kk < Cin && nn < g.Cout) ? ld4(g.pk + (int64_t)kk * g.Cout + nn) : f4(0.f);
+            const int kk = k0 + bq_k + (NT / NQ) * r, nn = n0 + 4 * bq_n;
+            bok[r] = kk < Cin && nn < g.Cout;
+            rb[r] = ld4(g.pk + (bok[r] ? (int64_t)kk * g.Cout + nn : 0));
         }
-        const int c = k0 + 4 * dq;  // depthwise taps of this thread's channel quad, prefetched
-#pragma unroll
-        for (int tp = 0; tp < 9; ++tp) rk[tp] = c < Cin ? ld4(g.dk + tp * Cin + c) : f4(0.f);
     };
-    auto store_stage = [&](int buf) {
-#pragma unroll
-        for (int j = 0; j < HR; ++j) {
-            const int e = tid + 256 * j;
-            if (e < NH) *reinterpret_cast<float4*>(&Xs[(e >> 2) * LR + 4 * (e & 3)]) = rh[j];
-        }
+    auto store_b = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r)
-            *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = rb[r];
+            *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (NT / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
     };
     // depthwise taps from the staged halo into the A tile: each thread evaluates one channel quad
-    // of two vertically adjacent pixels (4 halo rows x 3 columns of LDS reads for 2 outputs)
-    auto dw_stage = [&](int k0, int buf) {
-        float4 a0 = f4(0.f), a1 = f4(0.f);
+    // of RPT vertically adjacent pixels ((RPT + 2) x 3 LDS reads for RPT outputs)
+    const int dq = tid & 3;
+    const int dc = (tid >> 2) & 15, dr = RPT * (tid >> 6);
+    float4 ya[RPT];  // depthwise outputs of the last dw_stage (stored to y at the end of the iteration)
+    auto dw_stage = [&](int buf) {
+        const float* X = Xs[buf];
+        const float* Kt = Ks[buf];
+        float4 a[RPT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int o = 0; o < RPT; ++o) a[o] = f4(0.f);
+#pragma unroll
+        for (int i = 0; i < RPT + 2; ++i)
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj) {
-                const float4 xv = *reinterpret_cast<const float4*>(&Xs[((dr + i) * HWp + dc + jj) * LR + 4 * dq]);
-                if (i < 3) a0 = fma4(xv, rk[i * 3 + jj], a0);
-                if (i > 0) a1 = fma4(xv, rk[(i - 1) * 3 + jj], a1);
+                const float4 xv = *reinterpret_cast<const float4*>(&X[((dr + i) * HWp + dc + jj) * LR + 4 * dq]);
+#pragma unroll
+                for (int o = 0; o < RPT; ++o)
+                    if (i - o >= 0 && i - o < 3)
+                        a[o] = fma4(xv, *reinterpret_cast<const float4*>(&Kt[((i - o) * 3 + jj) * BK + 4 * dq]), a[o]);
             }
-        const int p0 = dr * TW + dc;
-        *reinterpret_cast<float4*>(&As[buf][p0 * LR + 4 * dq]) = a0;
-        *reinterpret_cast<float4*>(&As[buf][(p0 + TW) * LR + 4 * dq]) = a1;
+#pragma unroll
+        for (int o = 0; o < RPT; ++o) {
+            *reinterpret_cast<float4*>(&As[buf][((dr + o) * TW + dc) * LR + 4 * dq]) = a[o];
+            ya[o] = a[o];
+        }
+    };
+    auto store_y = [&](int k0) {
         if constexpr (WRITE_Y) {
             const int c = k0 + 4 * dq;
             if (blockIdx.y == 0 && c < Cin) {
                 float* yp = g.y + ((int64_t)(n * g.H + h0 + dr) * g.W + w0 + dc) * Cin + c;
-                st4(yp, a0);
-                st4(yp + (int64_t)g.W * Cin, a1);
+#pragma unroll
+                for (int o = 0; o < RPT; ++o) st4(yp + (int64_t)o * g.W * Cin, ya[o]);
             }
         }
     };
@@ -140,40 +225,51 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
+    auto mfma_kg = [&](int buf, int kg) {
+        float4 af[2], bf[TN];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+            af[tm] = *reinterpret_cast<const float4*>(&As[buf][(wm * 64 + tm * 32 + lo) * LR + kg * 8 + 4 * hi]);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const float* bp = &Bs[buf][(kg * 8 + 4 * hi) * LB + wn * (BN / WN) + tn * 32 + lo];
+            bf[tn] = make_float4(bp[0], bp[LB], bp[2 * LB], bp[3 * LB]);
+        }
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].x, bf[tn].x, acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].y, bf[tn].y, acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].z, bf[tn].z, acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].w, bf[tn].w, acc[tm][tn], 0, 0, 0);
+            }
+    };
+
     const int nk = (Cin + BK - 1) / BK;
-    load_stage(0);
-    store_stage(0);
+    // Loads past the last stage are issued from clamped (valid) addresses and their LDS images
+    // are never read, so the loop body is branch-free and the compiler's vmcnt counting stays
+    // exact (a conditional load forces a full drain at the join).
+    load_halo(0);
+    load_b(0);
+    store_halo(0);
+    store_b(0);
+    load_halo(BK);
+    store_halo(1);
     __syncthreads();
-    dw_stage(0, 0);
+    dw_stage(0);
+    store_y(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        const bool more = kt + 1 < nk;
-        if (more) load_stage((kt + 1) * BK);
-#pragma unroll
-        for (int kg = 0; kg < BK / 8; ++kg) {
-            float4 af[2], bf[TN];
-#pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
-                af[tm] = *reinterpret_cast<const float4*>(&As[buf][(wm * 64 + tm * 32 + lo) * LR + kg * 8 + 4 * hi]);
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const float* bp = &Bs[buf][(kg * 8 + 4 * hi) * LB + wn * (BN / 2) + tn * 32 + lo];
-                bf[tn] = make_float4(bp[0], bp[LB], bp[2 * LB], bp[3 * LB]);
-            }
-#pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) {
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].x, bf[tn].x, acc[tm][tn], 0, 0, 0);
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].y, bf[tn].y, acc[tm][tn], 0, 0, 0);
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].z, bf[tn].z, acc[tm][tn], 0, 0, 0);
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].w, bf[tn].w, acc[tm][tn], 0, 0, 0);
-                }
-        }
-        if (more) store_stage(buf ^ 1);  // Xs was last read by dw_stage(kt), before the last barrier
-        __syncthreads();
-        if (more) dw_stage((kt + 1) * BK, buf ^ 1);
+        load_halo((kt + 2) * BK);
+        load_b((kt + 1) * BK);
+        mfma_kg(buf, 0);
+        dw_stage(buf ^ 1);
+        mfma_kg(buf, 1);
+        store_halo(buf);  // halo kt was consumed by dw_stage in iteration kt-1
+        store_b(buf ^ 1);
+        if (kt + 1 < nk) store_y((kt + 1) * BK);
         __syncthreads();
     }
 
@@ -183,7 +279,7 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
     for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
-            const int col = n0 + wn * (BN / 2) + tn * 32 + lo;
+            const int col = n0 + wn * (BN / WN) + tn * 32 + lo;
             if (col >= g.Cout) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -196,7 +292,7 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
         float mean[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
-            const int cl = wn * (BN / 2) + tn * 32 + lo;
+            const int cl = wn * (BN / WN) + tn * 32 + lo;
             float s = 0.f;
 #pragma unroll
             for (int tm = 0; tm < 2; ++tm)
@@ -208,13 +304,13 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
         __syncthreads();
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
-            const int cl = wn * (BN / 2) + tn * 32 + lo;
+            const int cl = wn * (BN / WN) + tn * 32 + lo;
             mean[tn] = (red[cl] + red[BN + cl]) * (1.0f / 128.0f);
         }
         __syncthreads();
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
-            const int cl = wn * (BN / 2) + tn * 32 + lo;
+            const int cl = wn * (BN / WN) + tn * 32 + lo;
             float q = 0.f;
 #pragma unroll
             for (int tm = 0; tm < 2; ++tm)
@@ -233,7 +329,7 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
             // tile id (bn_finalize only needs 128-row counts, which all tiles have).
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
-                const int cl = wn * (BN / 2) + tn * 32 + lo;
+                const int cl = wn * (BN / WN) + tn * 32 + lo;
                 const int col = n0 + cl;
                 if (col < g.Cout)
                     g.stats[(int64_t)blockIdx.x * g.Cout + col] = make_float2(mean[tn], red[cl] + red[BN + cl]);
@@ -242,25 +338,32 @@ __global__ __launch_bounds__(256) void sepconv_fwd_kernel(SepArgs g) {
     }
 }
 
+template <int MODE, bool DROP, int BN, int WN>
+void launch_tile(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
+    const dim3 grid((unsigned)(a.N * (a.H / TH) * (a.W / TW)), (unsigned)cdiv(a.Cout, BN));
+    constexpr int NT = 128 * WN;
+    if (stats) {
+        if (write_y) sepconv_fwd_kernel<MODE, DROP, E_STATS, BN, WN, true><<<grid, NT, 0, st>>>(a);
+        else sepconv_fwd_kernel<MODE, DROP, E_STATS, BN, WN, false><<<grid, NT, 0, st>>>(a);
+    } else {
+        if (write_y) sepconv_fwd_kernel<MODE, DROP, E_STORE, BN, WN, true><<<grid, NT, 0, st>>>(a);
+        else sepconv_fwd_kernel<MODE, DROP, E_STORE, BN, WN, false><<<grid, NT, 0, st>>>(a);
+    }
+}
+
 template <int MODE, bool DROP>
 int launch(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
-    const unsigned tiles = (unsigned)(a.N * (a.H / TH) * (a.W / TW));
-#define UNET_SEP(BN_)                                                                                        \
-    {                                                                                                        \
-        dim3 grid(tiles, (unsigned)cdiv(a.Cout, BN_));                                                       \
-        if (stats) {                                                                                         \
-            if (write_y) sepconv_fwd_kernel<MODE, DROP, E_STATS, BN_, true><<<grid, 256, 0, st>>>(a);        \
-            else sepconv_fwd_kernel<MODE, DROP, E_STATS, BN_, false><<<grid, 256, 0, st>>>(a);               \
-        } else {                                                                                             \
-            if (write_y) sepconv_fwd_kernel<MODE, DROP, E_STORE, BN_, true><<<grid, 256, 0, st>>>(a);        \
-            else sepconv_fwd_kernel<MODE, DROP, E_STORE, BN_, false><<<grid, 256, 0, st>>>(a);               \
-        }                                                                                                    \
-    }
-    if (a.Cout <= 64)
-        UNET_SEP(64)
+    // the 256-wide, 8-wave tile when it still gives every CU (256) a block; else 128 (measured:
+    // tools/bench_sepconv.py, profiles/r1i_sepconv_bn_sweep.log)
+    const int64_t mt = (int64_t)a.N * (a.H / TH) * (a.W / TW);
+    int bn = a.Cout <= 64 ? 64 : a.Cout <= 128 ? 128 : 256;
+    if (bn == 256 && mt * cdiv(a.Cout, 256) < 256) bn = 128;
+    if (bn == 64)
+        launch_tile<MODE, DROP, 64, 2>(a, stats, write_y, st);
+    else if (bn == 128)
+        launch_tile<MODE, DROP, 128, 2>(a, stats, write_y, st);
     else
-        UNET_SEP(128)
-#undef UNET_SEP
+        launch_tile<MODE, DROP, 256, 4>(a, stats, write_y, st);
     UNET_CHECK_LAUNCH("unet_sepconv_fwd");
     return 0;
 }

@@ -127,9 +127,10 @@ class UNetEngine:
         # convolutions) runs on a second HIP stream, overlapping the data-gradient chain.
         self.side = torch.cuda.Stream(device=self.device)
         self.overlap = os.environ.get("UNET_OVERLAP", "1") != "0"  # 0: single stream (clean profiles)
-        # fused depthwise+pointwise forward: used where it measured faster than the two launches
-        # (tools/bench_sepconv.py: inference at >= 128x128; training keeps y, so the split path wins)
-        self.fuse_sepconv = "infer"
+        # Fused depthwise+pointwise forward (unet_sepconv_fwd) vs the two launches: "auto" uses it
+        # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
+        # profiles/r1i_sepconv_bn_sweep.log); "always" / "never" force the choice (tests).
+        self.fuse_sepconv = "auto"
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -224,7 +225,7 @@ class UNetEngine:
         gamma, beta, mm, mv = self._bn(b.name)
         dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
         pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
-        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "infer" and not training and h * w >= 128 * 128)
+        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= 64 * 64)
         if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight grad
             stats = training and self.use_bn
