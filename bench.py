@@ -31,6 +31,102 @@ PEAK_HBM_GBS = 8000.0
 ROOFLINE_OP = "unet_pointwise_fwd"
 
 
+RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # flop/B
+
+
+def roofline_obj(op, s, steps):
+    """Roofline object for one C-ABI op from KernelTimer totals (algorithmic flops / bytes)."""
+    sec = s["ms"] * 1e-3
+    mfma = s["bytes"] == 0 or s["flops"] / s["bytes"] >= RIDGE
+    if mfma:
+        ach, peak, unit = s["flops"] / sec / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
+    else:
+        ach, peak, unit = s["bytes"] / sec / 1e9, PEAK_HBM_GBS, "GB/s"
+    traffic, tsrc = pmc_traffic(op)
+    return {"bound": "mfma" if mfma else "hbm", "kernel": op, "achieved": round(ach, 2), "peak": peak,
+            "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+            "algorithmic_bytes_per_launch": round(s["bytes"] / s["launches"]),
+            "algorithmic_flops_per_launch": round(s["flops"] / s["launches"]),
+            "launches_per_step": s["launches"] // steps, "avg_launch_us": round(s["ms"] / s["launches"] * 1e3, 2)}
+
+
+def op_breakdown(summary):
+    """Per-op time of one step, largest first, with each op's roofline fraction."""
+    total = sum(d["ms"] for d in summary.values())
+    rows = []
+    for op, d in summary.items():
+        r = roofline_obj(op, d, 1)
+        rows.append({"op": op, "ms": round(d["ms"], 3), "share": round(d["ms"] / total, 4), "launches": d["launches"],
+                     "bound": r["bound"], "achieved": r["achieved"], "unit": r["unit"], "frac": r["frac"]})
+    rows.sort(key=lambda r: -r["ms"])
+    return rows
+
+
+def encoder_block_roofline(batch, size, device, reps=10):
+    """forward, training-mode conv blocks of the encoder (depthwise -> pointwise +
+    BN-statistics epilogue; the BN apply + ReLU of the input is done on load, as in the train
+    step) at `batch` images, each timed with HIP events (median of `reps`), against
+    t_roof = max(flops / peak_fp32, bytes / peak_hbm) with flops = px(18 Cin + 2 Cin Cout) and
+    bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Uses the engine's kernel choice
+    (fused unet_sepconv_fwd where supported, dw + pw launches for the 3-channel first block)."""
+    import torch
+    from unet_amd import ops
+    from unet_amd.ops import View
+    g = torch.Generator(device="cpu").manual_seed(7)
+    filters = (64, 128, 256, 512)
+    rows, cin, h = [], 3, size
+    for lvl, f in enumerate(filters):
+        for blk, (ci, co) in enumerate(((cin, f), (f, f))):
+            pool = lvl > 0 and blk == 0
+            hh = h
+            src = torch.rand((batch, 2 * hh if pool else hh, 2 * hh if pool else hh, ci), generator=g).to(device)
+            sc = torch.rand(ci, generator=g).to(device) + 0.5
+            sh = torch.randn(ci, generator=g).to(device) * 0.1
+            view = View.plain(src) if (lvl == 0 and blk == 0) else (View.pool_bnrelu(src, sc, sh) if pool
+                                                                     else View.bnrelu(src, sc, sh))
+            dk = torch.randn((3, 3, ci, 1), generator=g).to(device)
+            pk = (torch.randn((1, 1, ci, co), generator=g) / ci ** 0.5).to(device)
+            m = batch * hh * hh
+            ybuf = torch.empty((batch, hh, hh, ci), device=device)
+            z = torch.empty((batch, hh, hh, co), device=device)
+            part = torch.empty(ops.bn_partials_numel(m, co), device=device)
+            fused = ops.sepconv_supported(view, batch, hh, hh, co)
+
+            def run():
+                if fused:
+                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf, z, part)
+                else:
+                    ops.dwconv3x3_fwd(view, batch, hh, hh, dk, ybuf)
+                    ops.pointwise_fwd(ybuf, m, ci, co, pk, z, part)
+            for _ in range(3):
+                run()
+            ts = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                run()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3)
+            us = sorted(ts)[len(ts) // 2]
+            fl = m * (18.0 * ci + 2.0 * ci * co)
+            nb = 4.0 * (m * (ci + co) + 9 * ci + ci * co + 4 * co)
+            t_roof = max(fl / (PEAK_FP32_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)) * 1e6
+            rows.append({"block": f"enc{lvl + 1}_block{blk + 1}", "hw": hh, "cin": ci, "cout": co,
+                         "kernel": "unet_sepconv_fwd" if fused else "dwconv3x3_fwd+pointwise_fwd",
+                         "bound": "mfma" if fl / nb >= RIDGE else "hbm", "us": round(us, 1),
+                         "t_roof_us": round(t_roof, 1), "frac": round(t_roof / us, 4),
+                         "tflops": round(fl / us / 1e6, 1)})
+            del src, ybuf, z, part
+        cin, h = f, h // 2
+    mf = [r for r in rows if r["block"] >= "enc2"]
+    agg = sum(r["t_roof_us"] for r in mf) / sum(r["us"] for r in mf)
+    allf = sum(r["t_roof_us"] for r in rows) / sum(r["us"] for r in rows)
+    torch.cuda.empty_cache()
+    return {"batch": batch, "size": size, "blocks": rows, "frac_enc2_enc4": round(agg, 4),
+            "frac_all": round(allf, 4), "target": 0.90}
+
+
 def pmc_traffic(op):
     """HBM bytes per launch of `op` from the newest committed PMC summary (profiles/*_traffic.json,
     written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench)."""
@@ -98,6 +194,8 @@ def main():
     ap.add_argument("--num-classes", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--encoder-batch", type=int, default=32,
+                    help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -124,9 +222,22 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # one untimed single-stream step with every C-ABI op bracketed by HIP events: per-op
+    # breakdown, and the dominant op whose launches the timed region then measures (on the
+    # stream each launch is issued on) for the roofline object
+    breakdown, dominant = None, ROOFLINE_OP
     timer = None
     if not args.no_roofline:
-        timer = ops.KernelTimer([ROOFLINE_OP])
+        bt = ops.KernelTimer(None)
+        ops.TIMER = bt
+        overlap = model.engine.overlap
+        model.engine.overlap = False  # single stream: per-op times not inflated by the side stream
+        model.train_step(x, y)
+        model.engine.overlap = overlap
+        ops.TIMER = None
+        breakdown = op_breakdown(bt.summary())
+        dominant = breakdown[0]["op"]
+        timer = ops.KernelTimer([dominant])
         ops.TIMER = timer
     barrier()
     torch.cuda.synchronize()
@@ -167,19 +278,14 @@ def main():
             "final_loss": round(loss, 6),
         }
         if timer is not None:
-            s = timer.summary().get(ROOFLINE_OP)
+            s = timer.summary().get(dominant)
             if s:
-                avg_ms = s["ms"] / s["launches"]
-                ach = s["flops"] / (s["ms"] * 1e-3) / 1e12
-                traffic, tsrc = pmc_traffic(ROOFLINE_OP)
-                out["roofline"] = {"bound": "mfma", "kernel": ROOFLINE_OP, "achieved": round(ach, 2),
-                                   "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                                   "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                                   "traffic_source": tsrc,
-                                   "algorithmic_bytes_per_launch": round(s["bytes"] / s["launches"]),
-                                   "launches_per_step": s["launches"] // args.steps,
-                                   "avg_launch_us": round(avg_ms * 1e3, 2),
-                                   "algorithmic_gflop_per_step": round(s["flops"] / args.steps / 1e9, 3)}
+                out["roofline"] = roofline_obj(dominant, s, args.steps)
+                out["op_breakdown"] = breakdown[:8]
+        if not args.no_roofline and world == 1 and args.encoder_batch > 0:
+            del model
+            torch.cuda.empty_cache()
+            out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes)
         print(json.dumps(out), flush=True)

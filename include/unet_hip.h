@@ -153,6 +153,29 @@ int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int c,
                      uint64_t drop_seed, float* dgamma, float* dbeta,
                      float* dz, void* ws, size_t ws_bytes,
                      unet_stream_t stream);
+/* Statistics half of unet_bn_relu_bwd (same workspace): dgamma / dbeta and the
+ * per-channel coefficients coef[3c] = (mean, dbeta/M, rstd*dgamma/M) (zeros when
+ * use_bn == 0) with which unet_pointwise_bwd_data_bnrelu forms dz on load, so dz
+ * never takes a separate HBM pass.  Same reference lines as unet_bn_relu_bwd.     */
+int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c,
+                           const float* mean, const float* rstd,
+                           const float* scale, const float* shift, int use_bn,
+                           float drop_rate, uint64_t drop_seed, float* dgamma,
+                           float* dbeta, float* coef, void* ws, size_t ws_bytes,
+                           unet_stream_t stream);
+/* Pointwise data gradient of a conv_block whose output went through BN + ReLU
+ * (+ dropout): dz = scale*(g - coef_p - (z - coef_mu)*coef_q),
+ * g = da * keep/(1-rate) * [z*scale+shift > 0], is formed while loading the GEMM
+ * operand; dy[m, ci] = sum_co dz[m, co] * k[ci, co].  If dz != NULL the formed dz
+ * is also stored (the pointwise weight gradient reads it).  cin, cout % 4 == 0.
+ * Replaces the backward of model/u_net.py:20-25 (SeparableConv2D pointwise ->
+ * BatchNormalization -> ReLU) for the data path.                                 */
+int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m,
+                                   int cin, int cout, const float* pw_kernel,
+                                   const float* scale, const float* shift,
+                                   const float* coef, float drop_rate,
+                                   uint64_t drop_seed, float* dy, float* dz,
+                                   unet_stream_t stream);
 
 /* ----- Conv2DTranspose(f, 2, strides=2, padding='same') — u_net.py:88-94 --
  * out[n, 2i+a, 2j+b, co] = bias[co] + sum_ci x[n,i,j,ci] * k[a,b,co,ci];

@@ -46,16 +46,17 @@ def dropout_mult(seed: int, shape, rate: float, dtype=np.float64) -> np.ndarray:
     """Multiplier of keras.layers.Dropout(rate) in training (model/u_net.py:77-78, 97-98):
     keep with probability 1-rate, scale kept values by 1/(1-rate).  The Bernoulli draw is
     the engine's documented counter-based generator (TF's RNG stream is not reproducible
-    across frameworks): u(i) = (splitmix64(seed + i*golden) >> 40) / 2^24, keep iff u >= rate,
-    i = linear NHWC index of the element."""
+    across frameworks): for the linear NHWC index i of an element,
+    h = splitmix64(seed + (i >> 2)*golden), u(i) = ((h >> 16 (i & 3)) & 0xffff) / 2^16,
+    keep iff u >= rate (csrc/common.h: drop_mult)."""
     if rate <= 0.0:
         return np.ones(shape, dtype=dtype)
     n = int(np.prod(shape))
     idx = np.arange(n, dtype=np.uint64)
     with np.errstate(over="ignore"):
-        h = splitmix64(np.uint64(seed) + idx * _GOLDEN)
-    u = (h >> np.uint64(40)).astype(np.float64) * (1.0 / 16777216.0)
-    u32 = u.astype(np.float32)
+        h = splitmix64(np.uint64(seed) + (idx >> np.uint64(2)) * _GOLDEN)
+    bits = (h >> (np.uint64(16) * (idx & np.uint64(3)))) & np.uint64(0xFFFF)
+    u32 = bits.astype(np.float32) * np.float32(1.0 / 65536.0)
     keep = u32 >= np.float32(rate)
     inv_keep = np.float32(1.0) / (np.float32(1.0) - np.float32(rate))
     return np.where(keep, inv_keep, 0).astype(dtype).reshape(shape)

@@ -120,6 +120,7 @@ def test_train_step_parity(ncls, use_bn, drop, loss, fuse):
     n, hw = 2, 32
     model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
     model.engine.fuse_sepconv = fuse
+    model.engine.fuse_bn_bwd = fuse != "never"  # "never": also the separate BN-backward dz pass
     orc = UNetOracle(ncls, drop, use_bn)
     lr, wd = 2e-3, 1e-4
     okind = "dice" if loss == "dice_loss" else "iou"

@@ -199,6 +199,48 @@ def test_bn_relu_bwd(ops, use_bn, drop, m, c):
     assert rel_err(host(dz), rz.reshape(m, c)) < 1e-4
 
 
+@pytest.mark.parametrize("use_bn,drop", [(True, 0.0), (True, 0.2), (False, 0.0)])
+@pytest.mark.parametrize("m,cin,cout", [(300, 16, 32), (1000, 64, 128), (257, 128, 64), (128, 4, 8)])
+def test_pointwise_bwd_data_bnrelu(ops, use_bn, drop, m, cin, cout):
+    """BN + ReLU (+ dropout) backward folded into the pointwise data-gradient GEMM's operand load,
+    against the oracle's bn_relu_bwd followed by the pointwise backward."""
+    rng = np.random.default_rng(m + cin + 7 * cout)
+    c = cout
+    z = f32(rng.standard_normal((m, 1, 1, c)) * 2 + 0.3)
+    da = f32(rng.standard_normal((m, 1, 1, c)))
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cout))
+    gamma, beta = bn_affine(rng, c)
+    if use_bn:
+        _, mean, var = K.bn_train(z, gamma, beta)
+        rstd = 1 / np.sqrt(var + 1e-3)
+        scale = f32(gamma * rstd)
+        shift = f32(beta - mean * gamma * rstd)
+    else:
+        mean = var = rstd = np.zeros(c)
+        scale, shift = np.ones(c), beta
+    dmult = K.dropout_mult(55, da.shape, drop) if drop > 0 else None
+    dg = torch.zeros(c, device="cuda")
+    db = torch.zeros(c, device="cuda")
+    coef = torch.empty(3 * c, device="cuda")
+    ts, th = dev(scale), dev(shift)
+    ops.bn_relu_bwd_stats(dev(da), dev(z), m, c, dev(f32(mean)), dev(f32(rstd)), ts, th, use_bn, drop, 55,
+                          dg if use_bn else None, db, coef)
+    dy = torch.empty((m, cin), device="cuda")
+    dz = torch.full((m, c), 7.0, device="cuda")
+    ops.pointwise_bwd_data_bnrelu(dev(da), dev(z), m, cin, cout, dev(pk), ts, th, coef, drop, 55, dy, dz)
+    if use_bn:
+        rz, rg, rb = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var), drop=dmult)
+        assert rel_err(host(dg), rg) < 1e-4
+    else:
+        g = da if dmult is None else da * dmult
+        rz = np.where(z + beta > 0, g, 0)
+        rb = rz.reshape(-1, c).sum(0)
+    assert rel_err(host(db), rb) < 1e-5
+    assert rel_err(host(dz), rz.reshape(m, c)) < 1e-4
+    ry = rz.reshape(m, c) @ pk[0, 0].T
+    assert rel_err(host(dy), ry) < 1e-4
+
+
 @pytest.mark.parametrize("mode,drop", [(1, 0.0), (1, 0.2), (0, 0.0)])
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 4, 4, 64, 32), (2, 3, 5, 32, 16), (1, 8, 8, 128, 64)])
 def test_conv_transpose(ops, mode, drop, n, h, w, cin, cout):

@@ -5,5 +5,5 @@ TAG=${1:-run}
 run ops 600 python -m pytest tests/test_ops_gpu.py -q -x
 run model 900 python -m pytest tests/test_model_gpu.py -q -x
 if [ "$2" == "gemm" ]; then run gemm 600 python tools/bench_gemm.py; fi
-run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
-run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o $TAG -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline
+run bench 600 python bench.py --steps 20 --warmup 5
+run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o $TAG -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --encoder-batch 0

@@ -15,7 +15,9 @@ import sys
 
 # the kernels each C-ABI op launches (training-mode epilogues)
 OPS = {
-    "unet_pointwise_fwd": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 1, false>|gemm_rows_kernel<\d+, \d+, 0, false, 1>",
+    "unet_pointwise_fwd": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 1, (true|false)>|gemm_rows_kernel<\d+, \d+, 0, false, 1>",
+    "unet_pointwise_bwd_data": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 0, (true|false)>|gemm_rows_kernel<\d+, \d+, 0, false, 0>",
+    "unet_pointwise_bwd_filter": r"gemm_wgrad_(vec|kernel)<\d+, \d+, 0, false, 0, false>",
     "unet_sepconv_fwd": r"sepconv_fwd_kernel<",
 }
 

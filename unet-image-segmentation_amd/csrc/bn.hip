@@ -124,10 +124,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                 float4 g = ld4(da + m * C + c);
                 if constexpr (DROP) {
                     const uint64_t i = (uint64_t)m * C + c;
-                    g.x *= drop_mult(seed, i + 0, rate, inv_keep);
-                    g.y *= drop_mult(seed, i + 1, rate, inv_keep);
-                    g.z *= drop_mult(seed, i + 2, rate, inv_keep);
-                    g.w *= drop_mult(seed, i + 3, rate, inv_keep);
+                    g = mul4(g, drop_mult4(seed, i, rate, inv_keep));
                 }
                 g.x = fmaf(zz.x, s4.x, h4.x) > 0.f ? g.x : 0.f;
                 g.y = fmaf(zz.y, s4.y, h4.y) > 0.f ? g.y : 0.f;
@@ -190,10 +187,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
             float4 g = ld4(da + m * C + c);
             if constexpr (DROP) {
                 const uint64_t i = (uint64_t)m * C + c;
-                g.x *= drop_mult(seed, i + 0, rate, inv_keep);
-                g.y *= drop_mult(seed, i + 1, rate, inv_keep);
-                g.z *= drop_mult(seed, i + 2, rate, inv_keep);
-                g.w *= drop_mult(seed, i + 3, rate, inv_keep);
+                g = mul4(g, drop_mult4(seed, i, rate, inv_keep));
             }
             g.x = fmaf(zz.x, s4.x, h4.x) > 0.f ? g.x : 0.f;
             g.y = fmaf(zz.y, s4.y, h4.y) > 0.f ? g.y : 0.f;
@@ -228,6 +222,21 @@ __global__ void bn_bwd_store_kernel(const float* sums, int C, int use_bn, float*
     if (c >= C) return;
     if (dbeta) dbeta[c] = sums[c];
     if (use_bn && dgamma) dgamma[c] = sums[C + c];
+}
+
+// dbeta = S1, dgamma = S2 and the dz coefficients of A_BNBWD loads (gemm.hip):
+// coef = (mu, p, q) with p = S1 / M, q = rstd * S2 / M (zeros without BatchNorm: dz = g).
+__global__ void bn_bwd_coef_kernel(const float* sums, int C, int64_t M, int use_bn, const float* mean,
+                                   const float* rstd, float* dgamma, float* dbeta, float* coef) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float s1 = sums[c], s2 = sums[C + c];
+    if (dbeta) dbeta[c] = s1;
+    if (use_bn && dgamma) dgamma[c] = s2;
+    const float invM = 1.0f / (float)M;
+    coef[c] = use_bn ? mean[c] : 0.f;
+    coef[C + c] = use_bn ? s1 * invM : 0.f;
+    coef[2 * C + c] = use_bn ? rstd[c] * (s2 * invM) : 0.f;
 }
 
 template <bool VEC>
@@ -322,11 +331,12 @@ extern "C" size_t unet_bn_relu_bwd_workspace(int64_t m, int c) {
     return align_up((size_t)p.chunks * 2 * c * sizeof(float), 256) + align_up((size_t)2 * c * sizeof(float), 256);
 }
 
-extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int c, const float* mean,
-                                const float* rstd, const float* scale, const float* shift, int use_bn,
-                                float drop_rate, uint64_t drop_seed, float* dgamma, float* dbeta, float* dz,
-                                void* ws, size_t ws_bytes, unet_stream_t stream) {
-    UNET_CHECK_ARG(da && z && scale && shift && dz && m > 0 && c > 0, "unet_bn_relu_bwd: bad args");
+namespace {
+int bn_relu_bwd_impl(const float* da, const float* z, int64_t m, int c, const float* mean, const float* rstd,
+                     const float* scale, const float* shift, int use_bn, float drop_rate, uint64_t drop_seed,
+                     float* dgamma, float* dbeta, float* dz, float* coef_out, void* ws, size_t ws_bytes,
+                     unet_stream_t stream) {
+    UNET_CHECK_ARG(da && z && scale && shift && (dz || coef_out) && m > 0 && c > 0, "unet_bn_relu_bwd: bad args");
     UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_relu_bwd: use_bn needs mean/rstd");
     UNET_CHECK_ARG(drop_rate >= 0.f && drop_rate < 1.f, "unet_bn_relu_bwd: bad drop_rate");
     const size_t need = unet_bn_relu_bwd_workspace(m, c);
@@ -356,6 +366,12 @@ extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int 
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(reduce)");
     int rc = reduce_slabs(part, (int)p.chunks, (int64_t)2 * c, sums, (int64_t)2 * c, (int64_t)2 * c, st);
     if (rc) return rc;
+    if (coef_out) {  // statistics-only entry (unet_bn_relu_bwd_stats): no dz pass
+        bn_bwd_coef_kernel<<<(unsigned)cdiv(c, 256), 256, 0, st>>>(sums, c, m, use_bn, mean, rstd, dgamma, dbeta,
+                                                                    coef_out);
+        UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats(coef)");
+        return 0;
+    }
     bn_bwd_store_kernel<<<(unsigned)cdiv(c, 256), 256, 0, st>>>(sums, c, use_bn, dgamma, dbeta);
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(store)");
     const int64_t work = m * (vec ? c / 4 : c);
@@ -373,4 +389,23 @@ extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int 
 #undef UNET_BNA
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(apply)");
     return 0;
+}
+}  // namespace
+
+extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int c, const float* mean,
+                                const float* rstd, const float* scale, const float* shift, int use_bn,
+                                float drop_rate, uint64_t drop_seed, float* dgamma, float* dbeta, float* dz,
+                                void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(dz, "unet_bn_relu_bwd: null dz");
+    return bn_relu_bwd_impl(da, z, m, c, mean, rstd, scale, shift, use_bn, drop_rate, drop_seed, dgamma, dbeta, dz,
+                            nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c, const float* mean,
+                                      const float* rstd, const float* scale, const float* shift, int use_bn,
+                                      float drop_rate, uint64_t drop_seed, float* dgamma, float* dbeta, float* coef,
+                                      void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(coef, "unet_bn_relu_bwd_stats: null coef");
+    return bn_relu_bwd_impl(da, z, m, c, mean, rstd, scale, shift, use_bn, drop_rate, drop_seed, dgamma, dbeta,
+                            nullptr, coef, ws, ws_bytes, stream);
 }

@@ -65,17 +65,31 @@ __device__ __forceinline__ float bnrelu(float x, float sc, float sh) { return re
 __device__ __forceinline__ float4 bnrelu4(float4 x, float4 sc, float4 sh) { return relu4(fma4(x, sc, sh)); }
 
 // --------------------------------------------------------------- dropout ----
-// keep(i) <=> u(i) >= rate, u(i) = top 24 bits of splitmix64(seed + i*golden) / 2^24.
-// The oracle restates this bit-for-bit (oracle/keras_ops.py: dropout_keep).
+// Counter-based Bernoulli draw for the logical linear NHWC index i of an element: one splitmix64
+// per group of four consecutive elements, h = splitmix64(seed + (i >> 2) * golden); element i
+// takes the 16 bits (h >> 16 (i & 3)) & 0xffff, u = bits / 2^16, keep iff u >= rate.  A float4
+// of channels c..c+3 (c % 4 == 0, C % 4 == 0) costs one hash.  The oracle restates this
+// bit-for-bit (oracle/keras_ops.py: dropout_mult).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ float drop_mult(uint64_t seed, uint64_t idx, float rate, float inv_keep) {
-    uint64_t h = splitmix64(seed + idx * 0x9E3779B97F4A7C15ull);
-    float u = (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f);
+__device__ __forceinline__ uint64_t drop_hash(uint64_t seed, uint64_t group) {
+    return splitmix64(seed + group * 0x9E3779B97F4A7C15ull);
+}
+__device__ __forceinline__ float drop_bit(uint64_t h, int lane, float rate, float inv_keep) {
+    const float u = (float)((uint32_t)(h >> (16 * lane)) & 0xFFFFu) * (1.0f / 65536.0f);
     return u >= rate ? inv_keep : 0.f;
+}
+__device__ __forceinline__ float drop_mult(uint64_t seed, uint64_t idx, float rate, float inv_keep) {
+    return drop_bit(drop_hash(seed, idx >> 2), (int)(idx & 3), rate, inv_keep);
+}
+// multipliers of elements idx .. idx+3, idx % 4 == 0
+__device__ __forceinline__ float4 drop_mult4(uint64_t seed, uint64_t idx, float rate, float inv_keep) {
+    const uint64_t h = drop_hash(seed, idx >> 2);
+    return make_float4(drop_bit(h, 0, rate, inv_keep), drop_bit(h, 1, rate, inv_keep), drop_bit(h, 2, rate, inv_keep),
+                       drop_bit(h, 3, rate, inv_keep));
 }
 
 // ------------------------------------------------------------ reductions ----

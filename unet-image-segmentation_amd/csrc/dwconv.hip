@@ -28,10 +28,7 @@ __device__ __forceinline__ float4 tap4(const DView& v, int n, int hh, int ww, in
     float4 x = view_load4<MODE>(v, n, hh, ww, H, W, c);
     if constexpr (DROP) {
         const uint64_t i = ((uint64_t)((int64_t)(n * H + hh) * W + ww)) * v.C + c;
-        x.x *= drop_mult(v.seed, i + 0, v.rate, v.inv_keep);
-        x.y *= drop_mult(v.seed, i + 1, v.rate, v.inv_keep);
-        x.z *= drop_mult(v.seed, i + 2, v.rate, v.inv_keep);
-        x.w *= drop_mult(v.seed, i + 3, v.rate, v.inv_keep);
+        x = mul4(x, drop_mult4(v.seed, i, v.rate, v.inv_keep));
     }
     return x;
 }
@@ -123,10 +120,7 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_data_kernel(DView v, int N, i
             }
             if constexpr (DROP) {
                 const uint64_t li = (uint64_t)p * C + c;
-                acc.x *= drop_mult(v.seed, li + 0, v.rate, v.inv_keep);
-                acc.y *= drop_mult(v.seed, li + 1, v.rate, v.inv_keep);
-                acc.z *= drop_mult(v.seed, li + 2, v.rate, v.inv_keep);
-                acc.w *= drop_mult(v.seed, li + 3, v.rate, v.inv_keep);
+                acc = mul4(acc, drop_mult4(v.seed, li, v.rate, v.inv_keep));
             }
             if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
                 st4(dx0 + p * C + c, acc);

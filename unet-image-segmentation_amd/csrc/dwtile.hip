@@ -50,10 +50,7 @@ __device__ __forceinline__ void stage(float4* T, const DView& v, int n, int h0, 
             val = view_load4<MODE>(v, n, hh, ww, H, W, c);
             if constexpr (DROP) {
                 const uint64_t i = ((uint64_t)((n * H + hh) * W + ww)) * v.C + c;
-                val.x *= drop_mult(v.seed, i + 0, v.rate, v.inv_keep);
-                val.y *= drop_mult(v.seed, i + 1, v.rate, v.inv_keep);
-                val.z *= drop_mult(v.seed, i + 2, v.rate, v.inv_keep);
-                val.w *= drop_mult(v.seed, i + 3, v.rate, v.inv_keep);
+                val = mul4(val, drop_mult4(v.seed, i, v.rate, v.inv_keep));
             }
         }
         T[e] = val;
@@ -154,10 +151,7 @@ __global__ __launch_bounds__(256) void dw_tile_bwd_data(DView v, int N, int H, i
         const int p = (n * H + h) * W + w;
         if constexpr (DROP) {
             const uint64_t li = (uint64_t)p * C + c;
-            acc.x *= drop_mult(v.seed, li + 0, v.rate, v.inv_keep);
-            acc.y *= drop_mult(v.seed, li + 1, v.rate, v.inv_keep);
-            acc.z *= drop_mult(v.seed, li + 2, v.rate, v.inv_keep);
-            acc.w *= drop_mult(v.seed, li + 3, v.rate, v.inv_keep);
+            acc = mul4(acc, drop_mult4(v.seed, li, v.rate, v.inv_keep));
         }
         if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
             st4(dx0 + (int64_t)p * C + c, acc);

@@ -29,7 +29,10 @@ namespace {
 constexpr int BK = 16;
 constexpr int kStatsRows = 128;  // rows per BatchNorm partial (= BM of the stats GEMM)
 
-enum { A_PLAIN = 0, A_BNRELU = 1, A_UNSHUFFLE = 2 };
+// A_BNBWD: A = dz of a BatchNorm + ReLU (+ dropout) output, formed on load from the incoming
+// gradient da (a.src0) and the raw pre-BN z: g = da * drop * [z*sc+sh > 0],
+// dz = sc * (g - p - (z - mu) * q) with per-channel (mu, p, q) = coef[0..3C) (see bn.hip).
+enum { A_PLAIN = 0, A_BNRELU = 1, A_UNSHUFFLE = 2, A_BNBWD = 3 };
 enum { E_STORE = 0, E_STATS = 1, E_SHUFFLE = 2 };
 
 struct RowsArgs {
@@ -45,6 +48,9 @@ struct RowsArgs {
     const float* bias;
     float2* stats;
     int sH, sW, sf;  // SHUFFLE epilogue: m = (n, i, j) over sH x sW, out (n, 2sH, 2sW, sf)
+    const float* z;     // A_BNBWD: pre-BN z (same layout as a.src0)
+    const float* coef;  // A_BNBWD: (mu, p, q) x C
+    float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
 };
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
@@ -474,55 +480,80 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         }
     }
 
+    // Loads are issued unconditionally from clamped addresses; validity masks, the view
+    // transform and dropout are applied when the registers are written to LDS, so no load is
+    // waited for before the stage's MFMAs.
     float4 ra[AQ], rb[BQ];
+    float4 rz[AMODE == A_BNBWD ? AQ : 1];
+    float4 csc, csh, cmu, cp, cq;  // per-stage channel constants of this thread's k-quad
+    int ak = 0;                    // k of this thread's A quad in the staged k-stage
+    bool bok[BQ];
     auto load_stage = [&](int k0) {
         const int k = k0 + 4 * kq;
-        const bool kv = k < K;
-        int koff = k;
-        float4 sc = f4(1.f), sh = f4(0.f);
+        ak = k;
+        const int kc = k < K ? k : 0;
+        int koff = kc;
         if constexpr (AMODE == A_UNSHUFFLE) {
-            const int ab = k / g.uf;
-            const int co = k - ab * g.uf;
+            const int ab = kc / g.uf;
+            const int co = kc - ab * g.uf;
             koff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
         }
-        if constexpr (AMODE == A_BNRELU) {
-            if (kv) {
-                sc = ld4(g.a.sc0 + k);
-                sh = ld4(g.a.sh0 + k);
-            }
+        if constexpr (AMODE == A_BNRELU || AMODE == A_BNBWD) {
+            csc = ld4(g.a.sc0 + kc);
+            csh = ld4(g.a.sh0 + kc);
+        }
+        if constexpr (AMODE == A_BNBWD) {
+            cmu = ld4(g.coef + kc);
+            cp = ld4(g.coef + K + kc);
+            cq = ld4(g.coef + 2 * K + kc);
         }
 #pragma unroll
         for (int r = 0; r < AQ; ++r) {
-            float4 v = f4(0.f);
-            if (kv && aoff[r] >= 0) {
-                v = ld4(g.a.src0 + aoff[r] + koff);
-                if constexpr (AMODE == A_BNRELU) v = bnrelu4(v, sc, sh);
-                if constexpr (DROP) {
-                    const uint64_t i = (uint64_t)(m0 + arow + (256 / KQ) * r) * g.a.C + k;
-                    v.x *= drop_mult(g.a.seed, i + 0, g.a.rate, g.a.inv_keep);
-                    v.y *= drop_mult(g.a.seed, i + 1, g.a.rate, g.a.inv_keep);
-                    v.z *= drop_mult(g.a.seed, i + 2, g.a.rate, g.a.inv_keep);
-                    v.w *= drop_mult(g.a.seed, i + 3, g.a.rate, g.a.inv_keep);
-                }
-            }
-            ra[r] = v;
+            const int o = (aoff[r] < 0 ? 0 : aoff[r]) + koff;
+            ra[r] = ld4(g.a.src0 + o);
+            if constexpr (AMODE == A_BNBWD) rz[r] = ld4(g.z + o);
         }
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const int kk = BKC ? k0 + 4 * bq_k : k0 + bq_k + (256 / NQ) * r;
-            rb[r] = (boff[r] >= 0 && kk < K) ? ld4(g.B + boff[r] + (BKC ? k0 : k0 * sbk)) : f4(0.f);
+            bok[r] = boff[r] >= 0 && kk < K;
+            rb[r] = ld4(g.B + (bok[r] ? boff[r] + (BKC ? k0 : k0 * sbk) : 0));
         }
     };
     auto store_stage = [&](int buf) {
+        const bool kv = ak < K;
 #pragma unroll
-        for (int r = 0; r < AQ; ++r)
-            *reinterpret_cast<float4*>(&As[buf][(arow + (256 / KQ) * r) * LR + 4 * kq]) = ra[r];
+        for (int r = 0; r < AQ; ++r) {
+            float4 v = ra[r];
+            if constexpr (AMODE == A_BNRELU) v = bnrelu4(v, csc, csh);
+            if constexpr (DROP) {
+                const uint64_t i = (uint64_t)(m0 + arow + (256 / KQ) * r) * g.a.C + (kv ? ak : 0);
+                v = mul4(v, drop_mult4(g.a.seed, i, g.a.rate, g.a.inv_keep));
+            }
+            if constexpr (AMODE == A_BNBWD) {
+                const float4 zz = rz[r];
+                v.x = fmaf(zz.x, csc.x, csh.x) > 0.f ? v.x : 0.f;
+                v.y = fmaf(zz.y, csc.y, csh.y) > 0.f ? v.y : 0.f;
+                v.z = fmaf(zz.z, csc.z, csh.z) > 0.f ? v.z : 0.f;
+                v.w = fmaf(zz.w, csc.w, csh.w) > 0.f ? v.w : 0.f;
+                v.x = csc.x * (v.x - cp.x - (zz.x - cmu.x) * cq.x);
+                v.y = csc.y * (v.y - cp.y - (zz.y - cmu.y) * cq.y);
+                v.z = csc.z * (v.z - cp.z - (zz.z - cmu.z) * cq.z);
+                v.w = csc.w * (v.w - cp.w - (zz.w - cmu.w) * cq.w);
+            }
+            if (!kv || aoff[r] < 0) v = f4(0.f);
+            if constexpr (AMODE == A_BNBWD) {
+                if (g.side && blockIdx.y == 0 && kv && aoff[r] >= 0) st4(g.side + aoff[r] + ak, v);
+            }
+            *reinterpret_cast<float4*>(&As[buf][(arow + (256 / KQ) * r) * LR + 4 * kq]) = v;
+        }
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
+            const float4 v = bok[r] ? rb[r] : f4(0.f);
             if constexpr (BKC)
-                *reinterpret_cast<float4*>(&Bs[buf][(bq_n + (256 / KQ) * r) * LR + 4 * bq_k]) = rb[r];
+                *reinterpret_cast<float4*>(&Bs[buf][(bq_n + (256 / KQ) * r) * LR + 4 * bq_k]) = v;
             else
-                *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = rb[r];
+                *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = v;
         }
     };
 
@@ -728,10 +759,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
                     if constexpr (AMODE == W_BNRELU) v = bnrelu4(v, asc, ash);
                     if constexpr (ADROP) {
                         const uint64_t i = (uint64_t)m * g.a.C + p;
-                        v.x *= drop_mult(g.a.seed, i + 0, g.a.rate, g.a.inv_keep);
-                        v.y *= drop_mult(g.a.seed, i + 1, g.a.rate, g.a.inv_keep);
-                        v.z *= drop_mult(g.a.seed, i + 2, g.a.rate, g.a.inv_keep);
-                        v.w *= drop_mult(g.a.seed, i + 3, g.a.rate, g.a.inv_keep);
+                        v = mul4(v, drop_mult4(g.a.seed, i, g.a.rate, g.a.inv_keep));
                     }
                 }
             }
@@ -746,10 +774,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
                 if constexpr (BMODE == W_BNRELU) v = bnrelu4(v, bsc, bsh);
                 if constexpr (BDROP) {
                     const uint64_t i = (uint64_t)m * g.b.C + q;
-                    v.x *= drop_mult(g.b.seed, i + 0, g.b.rate, g.b.inv_keep);
-                    v.y *= drop_mult(g.b.seed, i + 1, g.b.rate, g.b.inv_keep);
-                    v.z *= drop_mult(g.b.seed, i + 2, g.b.rate, g.b.inv_keep);
-                    v.w *= drop_mult(g.b.seed, i + 3, g.b.rate, g.b.inv_keep);
+                    v = mul4(v, drop_mult4(g.b.seed, i, g.b.rate, g.b.inv_keep));
                 }
             }
             rb[r] = v;
@@ -823,6 +848,21 @@ bool rows_vec_ok(const RowsArgs& a, int amode) {
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     const unsigned gm = (unsigned)cdiv(a.M, 128);
+    if constexpr (AMODE == A_BNBWD) {  // vectorised kernel only
+        UNET_CHECK_ARG(rows_vec_ok(a, AMODE), "%s: needs channel counts divisible by 4 and 16-B aligned operands",
+                       what);
+        if (a.N <= 64) {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 64));
+            if (a.sbk == 1) gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
+            else gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
+        } else {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 128));
+            if (a.sbk == 1) gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
+            else gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
+        }
+        UNET_CHECK_LAUNCH(what);
+        return 0;
+    } else {
     if (rows_vec_ok(a, AMODE)) {
         const bool bkc = a.sbk == 1;
         if (a.N <= 64) {
@@ -846,6 +886,7 @@ int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     }
     UNET_CHECK_LAUNCH(what);
     return 0;
+    }
 }
 
 struct WgradPlan {
@@ -990,6 +1031,40 @@ extern "C" int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int 
     a.C = dy;
     a.ldc = cin;
     return launch_rows<A_PLAIN, false, E_STORE>(a, as_stream(stream), "unet_pointwise_bwd_data");
+}
+
+extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout,
+                                              const float* pw_kernel, const float* scale, const float* shift,
+                                              const float* coef, float drop_rate, uint64_t drop_seed, float* dy,
+                                              float* dz, unet_stream_t stream) {
+    UNET_CHECK_ARG(da && z && pw_kernel && scale && shift && coef && dy, "unet_pointwise_bwd_data_bnrelu: null pointer");
+    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_data_bnrelu: bad sizes");
+    UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_bwd_data_bnrelu: tensor too large");
+    UNET_CHECK_ARG(drop_rate >= 0.f && drop_rate < 1.f, "unet_pointwise_bwd_data_bnrelu: bad drop_rate");
+    UNET_CHECK_ARG(((uintptr_t)z | (uintptr_t)coef | (uintptr_t)scale | (uintptr_t)shift | (uintptr_t)dz) % 16 == 0,
+                   "unet_pointwise_bwd_data_bnrelu: operands must be 16-B aligned");
+    RowsArgs a{};
+    a.a = plain_view(da, cout);
+    a.a.sc0 = scale;
+    a.a.sh0 = shift;
+    a.a.rate = drop_rate;
+    a.a.inv_keep = drop_rate > 0.f ? 1.0f / (1.0f - drop_rate) : 1.0f;
+    a.a.seed = drop_seed;
+    a.z = z;
+    a.coef = coef;
+    a.side = dz;
+    a.M = m;
+    a.K = cout;
+    a.B = pw_kernel;  // B(k = co, n = ci) = k[ci][co]
+    a.sbk = 1;
+    a.sbn = cout;
+    a.N = cin;
+    a.C = dy;
+    a.ldc = cin;
+    hipStream_t st = as_stream(stream);
+    if (drop_rate > 0.f)
+        return launch_rows<A_BNBWD, true, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
+    return launch_rows<A_BNBWD, false, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
 }
 
 extern "C" size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout) {

@@ -152,10 +152,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
             }
             if constexpr (DROP) {
                 const uint64_t i = (uint64_t)(lp[j] < 0 ? 0 : lp[j]) * C + hc;
-                v.x *= drop_mult(g.x.seed, i + 0, g.x.rate, g.x.inv_keep);
-                v.y *= drop_mult(g.x.seed, i + 1, g.x.rate, g.x.inv_keep);
-                v.z *= drop_mult(g.x.seed, i + 2, g.x.rate, g.x.inv_keep);
-                v.w *= drop_mult(g.x.seed, i + 3, g.x.rate, g.x.inv_keep);
+                v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
             }
             if (lp[j] < 0 || !cok) v = f4(0.f);
             if (e < NH) *reinterpret_cast<float4*>(&Xs[buf][(e >> 2) * LR + 4 * (e & 3)]) = v;

@@ -95,10 +95,7 @@ __device__ __forceinline__ float4 row_load4(const DView& v, int64_t m, int c) {
     if constexpr (MODE == UNET_VIEW_BNRELU) x = bnrelu4(x, ld4(v.sc0 + c), ld4(v.sh0 + c));
     if constexpr (DROP) {
         const uint64_t i = (uint64_t)m * v.C + c;
-        x.x *= drop_mult(v.seed, i + 0, v.rate, v.inv_keep);
-        x.y *= drop_mult(v.seed, i + 1, v.rate, v.inv_keep);
-        x.z *= drop_mult(v.seed, i + 2, v.rate, v.inv_keep);
-        x.w *= drop_mult(v.seed, i + 3, v.rate, v.inv_keep);
+        x = mul4(x, drop_mult4(v.seed, i, v.rate, v.inv_keep));
     }
     return x;
 }

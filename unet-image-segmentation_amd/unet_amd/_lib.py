@@ -61,6 +61,10 @@ SIGNATURES = {
     "unet_bn_relu_bwd_workspace": (c_size_t, [c_int64, c_int]),
     "unet_bn_relu_bwd": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                  c_size_t, P]),
+    "unet_bn_relu_bwd_stats": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
+                                       c_size_t, P]),
+    "unet_pointwise_bwd_data_bnrelu": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, c_float, c_uint64, P, P,
+                                               P]),
     "unet_conv_transpose2x2_fwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P]),
     "unet_conv_transpose2x2_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_conv_transpose2x2_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),

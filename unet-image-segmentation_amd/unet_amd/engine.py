@@ -67,6 +67,7 @@ class BlockBufs:
     da: torch.Tensor  # gradient w.r.t. this block's output activation
     dz: Optional[torch.Tensor] = None  # backward-only, allocated on first backward
     dy: Optional[torch.Tensor] = None
+    coef: Optional[torch.Tensor] = None  # BN-backward coefficients (mean, dbeta/M, rstd*dgamma/M)
 
 
 @dataclass
@@ -131,6 +132,8 @@ class UNetEngine:
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
         # profiles/r1i_sepconv_bn_sweep.log); "always" / "never" force the choice (tests).
         self.fuse_sepconv = "auto"
+        # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
+        self.fuse_bn_bwd = True
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -313,16 +316,24 @@ class UNetEngine:
         if bb.dz is None:
             bb.dz = torch.empty(m * b.cout, dtype=torch.float32, device=self.device)
             bb.dy = torch.empty(m * b.cin, dtype=torch.float32, device=self.device)
+            bb.coef = torch.empty(3 * b.cout, dtype=torch.float32, device=self.device)
         dz, dy = bb.dz, bb.dy
         if self.use_bn:
             dgamma, dbeta = self.gvars[f"{b.name}_bn/gamma"], self.gvars[f"{b.name}_bn/beta"]
         else:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
-        ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
-                        drop_seed, dgamma, dbeta, dz)
         pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
         dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
-        ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
+        if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
+            # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
+            ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
+                                  drop_rate, drop_seed, dgamma, dbeta, bb.coef)
+            ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef, drop_rate,
+                                          drop_seed, dy, dz)
+        else:
+            ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
+                            drop_seed, dgamma, dbeta, dz)
+            ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gpk = self.gvars[f"{b.name}_sepconv/pointwise_kernel"]
         gdk = self.gvars[f"{b.name}_sepconv/depthwise_kernel"]
         if self.overlap:  # weight gradients off the critical path, on the side stream

@@ -63,8 +63,8 @@ class KernelTimer:
     (torch's current stream) and accumulates their algorithmic flops / bytes, so a bench
     can report achieved throughput of one kernel over a timed region."""
 
-    def __init__(self, names):
-        self.names = set(names)
+    def __init__(self, names=None):
+        self.names = None if names is None else set(names)  # None: every op
         self.records = []  # (name, flops, bytes, start_event, end_event)
 
     def summary(self):
@@ -85,7 +85,7 @@ TIMER: Optional[KernelTimer] = None
 def _call(name: str, work, *args):
     """L.call, bracketed by HIP events when TIMER selects `name`; work = (flops, bytes)."""
     t = TIMER
-    if t is None or name not in t.names:
+    if t is None or (t.names is not None and name not in t.names):
         L.call(name, *args)
         return
     e0 = torch.cuda.Event(enable_timing=True)
@@ -140,6 +140,13 @@ class View:
     def concat(up: Tensor, skip_z: Tensor, scale: Tensor, shift: Tensor) -> "View":
         return View(L.VIEW_CONCAT, up, up.shape[-1], None, None, skip_z, skip_z.shape[-1], scale, shift)
 
+    def src_bytes(self, n: int, h: int, w: int) -> float:
+        """Algorithmic bytes of one pass over the view's sources at logical size (n, h, w)."""
+        px = float(n * h * w)
+        if self.mode == L.VIEW_POOL_BNRELU:
+            return 16.0 * px * self.c0
+        return 4.0 * px * self.channels
+
     def dropout(self, rate: float, seed: int) -> "View":
         return replace(self, drop_rate=float(rate), drop_seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
 
@@ -166,7 +173,8 @@ class View:
 def view_materialize(x: View, n: int, h: int, w: int, out: Tensor) -> Tensor:
     _check(out, "out", n * h * w * x.channels)
     vs = x.c_struct()
-    L.call("unet_view_materialize", ctypes.byref(vs), n, h, w, _ptr(out), _stream())
+    _call("unet_view_materialize", (0.0, x.src_bytes(n, h, w) + 4.0 * out.numel()), ctypes.byref(vs), n, h, w,
+          _ptr(out), _stream())
     return out
 
 
@@ -176,8 +184,8 @@ def dwconv3x3_fwd(x: View, n: int, h: int, w: int, dk: Tensor, out: Tensor) -> T
     _check(dk, "depthwise_kernel", 9 * C)
     _check(out, "out", n * h * w * C)
     vs = x.c_struct()
-    _call("unet_dwconv3x3_fwd", (18.0 * n * h * w * C, 4.0 * (2 * n * h * w * C + 9 * C)), ctypes.byref(vs), n, h,
-          w, _ptr(dk), _ptr(out), _stream())
+    _call("unet_dwconv3x3_fwd", (18.0 * n * h * w * C, x.src_bytes(n, h, w) + 4.0 * (n * h * w * C + 9 * C)),
+          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(out), _stream())
     return out
 
 
@@ -189,8 +197,11 @@ def dwconv3x3_bwd_data(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Tensor, dx
     if dx1 is not None:
         _check(dx1, "dx1")
     vs = x.c_struct()
-    L.call("unet_dwconv3x3_bwd_data", ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dx0), _ptr(dx1),
-           _stream())
+    m = n * h * w
+    # read dy, write dx; the pool route also reads the 2x2 sources and read-modify-writes dx0
+    nb = 8.0 * m * C + (3.0 * x.src_bytes(n, h, w) if x.mode == L.VIEW_POOL_BNRELU else 0.0)
+    _call("unet_dwconv3x3_bwd_data", (18.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dx0),
+          _ptr(dx1), _stream())
 
 
 def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
@@ -199,7 +210,8 @@ def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
     _check(ddk, "d_depthwise_kernel", 9 * C)
     ws, wsb = _ws(L.query("unet_dwconv3x3_bwd_filter_workspace", n, h, w, C), dy.device)
     vs = x.c_struct()
-    L.call("unet_dwconv3x3_bwd_filter", ctypes.byref(vs), n, h, w, _ptr(dy), _ptr(ddk), ws, wsb, _stream())
+    _call("unet_dwconv3x3_bwd_filter", (18.0 * n * h * w * C, x.src_bytes(n, h, w) + 4.0 * n * h * w * C),
+          ctypes.byref(vs), n, h, w, _ptr(dy), _ptr(ddk), ws, wsb, _stream())
 
 
 def bn_partials_numel(m: int, c: int) -> int:
@@ -251,20 +263,21 @@ def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tens
     if partials is not None:
         _check(partials, "bn_partials", bn_partials_numel(m, cout))
     vs = x.c_struct()
-    _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C, 4.0 * (m * C + m * cout + C * cout)),
+    _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C,
+                               x.src_bytes(n, h, w) + 4.0 * (m * cout + C * cout + 9 * C)),
           ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _stream())
 
 
 # ------------------------------------------------------------------ BatchNorm ---
 def bn_finalize(partials: Tensor, m: int, c: int, gamma, beta, eps, momentum, moving_mean, moving_var,
                 update_moving: bool, mean, rstd, scale, shift):
-    L.call("unet_bn_finalize", _ptr(partials), m, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+    _call("unet_bn_finalize", (0.0, 8.0 * bn_partials_numel(m, c) / 2), _ptr(partials), m, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
            _ptr(moving_mean), _ptr(moving_var), int(bool(update_moving)), _ptr(mean), _ptr(rstd), _ptr(scale),
            _ptr(shift), _stream())
 
 
 def bn_infer_params(gamma, beta, moving_mean, moving_var, c: int, eps, scale: Tensor, shift: Tensor):
-    L.call("unet_bn_infer_params", _ptr(gamma), _ptr(beta), _ptr(moving_mean), _ptr(moving_var), c, float(eps),
+    _call("unet_bn_infer_params", (0.0, 24.0 * c), _ptr(gamma), _ptr(beta), _ptr(moving_mean), _ptr(moving_var), c, float(eps),
            _ptr(scale), _ptr(shift), _stream())
 
 
@@ -274,9 +287,38 @@ def bn_relu_bwd(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, shift,
     _check(z, "z", m * c)
     _check(dz, "dz", m * c)
     ws, wsb = _ws(L.query("unet_bn_relu_bwd_workspace", m, c), z.device)
-    L.call("unet_bn_relu_bwd", _ptr(da), _ptr(z), m, c, _ptr(mean), _ptr(rstd), _ptr(scale), _ptr(shift),
+    _call("unet_bn_relu_bwd", (12.0 * m * c, 12.0 * m * c), _ptr(da), _ptr(z), m, c, _ptr(mean), _ptr(rstd), _ptr(scale), _ptr(shift),
            int(bool(use_bn)), float(drop_rate), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dgamma), _ptr(dbeta),
            _ptr(dz), ws, wsb, _stream())
+
+
+def bn_relu_bwd_stats(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, shift, use_bn: bool,
+                      drop_rate: float, drop_seed: int, dgamma, dbeta, coef: Tensor):
+    """Statistics half of bn_relu_bwd: dgamma / dbeta and coef (3c) for pointwise_bwd_data_bnrelu."""
+    _check(da, "da", m * c)
+    _check(z, "z", m * c)
+    _check(coef, "coef", 3 * c)
+    ws, wsb = _ws(L.query("unet_bn_relu_bwd_workspace", m, c), z.device)
+    _call("unet_bn_relu_bwd_stats", (8.0 * m * c, 8.0 * m * c), _ptr(da), _ptr(z), m, c, _ptr(mean), _ptr(rstd),
+          _ptr(scale), _ptr(shift), int(bool(use_bn)), float(drop_rate), int(drop_seed) & 0xFFFFFFFFFFFFFFFF,
+          _ptr(dgamma), _ptr(dbeta), _ptr(coef), ws, wsb, _stream())
+
+
+def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
+                              shift: Tensor, coef: Tensor, drop_rate: float, drop_seed: int, dy: Tensor,
+                              dz: Optional[Tensor]):
+    """dy = dz . pk^T with dz (BN + ReLU + dropout backward) formed on load; optionally stores dz."""
+    _check(da, "da", m * cout)
+    _check(z, "z", m * cout)
+    _check(pk, "pointwise_kernel", cin * cout)
+    _check(coef, "coef", 3 * cout)
+    _check(dy, "dy", m * cin)
+    if dz is not None:
+        _check(dz, "dz", m * cout)
+    _call("unet_pointwise_bwd_data_bnrelu",
+          (2.0 * m * cin * cout, 4.0 * (2 * m * cout + m * cin + cin * cout) + (4.0 * m * cout if dz is not None else 0)),
+          _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), float(drop_rate),
+          int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream())
 
 
 # ------------------------------------------------------------ Conv2DTranspose ---
@@ -298,7 +340,10 @@ def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: O
         _check(dx, "dx", n * h * w * x.c0)
     ws, wsb = _ws(L.query("unet_conv_transpose2x2_bwd_workspace", n, h, w, x.c0, cout), dout.device)
     vs = x.c_struct()
-    L.call("unet_conv_transpose2x2_bwd", ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(dout), _ptr(dx), _ptr(dk),
+    m = n * h * w
+    fl = (16.0 if dx is not None else 8.0) * m * x.c0 * cout  # dgrad + wgrad
+    nb = x.src_bytes(n, h, w) + 16.0 * m * cout + (4.0 * m * x.c0 if dx is not None else 0.0) + 32.0 * x.c0 * cout
+    _call("unet_conv_transpose2x2_bwd", (fl, nb), ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(dout), _ptr(dx), _ptr(dk),
            _ptr(db), ws, wsb, _stream())
 
 
@@ -307,7 +352,8 @@ def head_fwd(x: View, n, h, w, ncls, k: Tensor, b: Optional[Tensor], prob: Tenso
     _check(k, "kernel", x.c0 * ncls)
     _check(prob, "prob", n * h * w * ncls)
     vs = x.c_struct()
-    L.call("unet_head_fwd", ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(b), _ptr(prob), _stream())
+    _call("unet_head_fwd", (2.0 * n * h * w * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * n * h * w * ncls),
+          ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(b), _ptr(prob), _stream())
 
 
 def dice_fwd(y_true: Tensor, y_pred: Tensor, n: int, hw: int, ncls: int, smooth: float, sums: Optional[Tensor],
@@ -318,7 +364,7 @@ def dice_fwd(y_true: Tensor, y_pred: Tensor, n: int, hw: int, ncls: int, smooth:
     if sums is not None:
         _check(sums, "sums", n * ncls * 3)
     ws, wsb = _ws(L.query("unet_dice_workspace", n, hw, ncls), y_pred.device)
-    L.call("unet_dice_fwd", _ptr(y_true), _ptr(y_pred), n, hw, ncls, float(smooth), _ptr(sums), _ptr(result), ws,
+    _call("unet_dice_fwd", (4.0 * n * hw * ncls, 8.0 * n * hw * ncls), _ptr(y_true), _ptr(y_pred), n, hw, ncls, float(smooth), _ptr(sums), _ptr(result), ws,
            wsb, _stream())
 
 
@@ -329,7 +375,9 @@ def head_bwd(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, su
     _check(dx, "dx", n * h * w * x.c0)
     ws, wsb = _ws(L.query("unet_head_bwd_workspace", n, h, w, x.c0, ncls), prob.device)
     vs = x.c_struct()
-    L.call("unet_head_bwd", ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums),
+    m = n * h * w
+    _call("unet_head_bwd", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
+          ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums),
            float(smooth), int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), ws, wsb, _stream())
 
 
@@ -342,7 +390,7 @@ def meaniou_update(y_true: Tensor, y_pred: Tensor, num_classes: int, threshold: 
     thr = -1.0 if threshold is None else float(threshold)
     if threshold is not None and threshold < 0:
         raise ValueError("threshold must be >= 0")
-    L.call("unet_meaniou_update", _ptr(y_true), _ptr(y_pred), y_true.numel(), num_classes, thr, _ptr(confusion),
+    _call("unet_meaniou_update", (0.0, 8.0 * y_true.numel()), _ptr(y_true), _ptr(y_pred), y_true.numel(), num_classes, thr, _ptr(confusion),
            _stream())
 
 
@@ -350,5 +398,5 @@ def adamw_step(param: Tensor, grad: Tensor, m: Tensor, v: Tensor, lr, wd, b1, b2
     n = param.numel()
     for t, nm in ((param, "param"), (grad, "grad"), (m, "m"), (v, "v")):
         _check(t, nm, n)
-    L.call("unet_adamw_step", _ptr(param), _ptr(grad), _ptr(m), _ptr(v), n, float(lr), float(wd), float(b1),
+    _call("unet_adamw_step", (20.0 * n, 28.0 * n), _ptr(param), _ptr(grad), _ptr(m), _ptr(v), n, float(lr), float(wd), float(b1),
            float(b2), float(eps), float(alpha), float(grad_scale), _stream())
