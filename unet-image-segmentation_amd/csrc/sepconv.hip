@@ -18,7 +18,8 @@ namespace {
 constexpr int TH = 8, TW = 16;            // pixel rectangle of one M tile
 constexpr int HHp = TH + 2, HWp = TW + 2; // halo
 constexpr int BK = 16;                    // channels per k-stage
-constexpr int LR = BK + 4;                // LDS row stride (floats) of A / halo / k-contiguous B
+constexpr int LR = BK + 4;                // LDS row stride (floats) of the A tile (conflict-free fragments)
+constexpr int XLR = BK;                   // halo pixel stride: lane-linear, conflict-free b128 reads
 enum { E_STORE = 0, E_STATS = 1 };
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
@@ -36,8 +37,12 @@ struct SepArgs {
 // WN = waves along N (2 or 4); the block has 2 x WN waves, each owning a 64 x (BN / WN) piece of
 // the 128 x BN output tile.  Wide tiles (BN = 256, 8 waves) give two waves per SIMD, so one wave's
 // halo / depthwise work overlaps the other's MFMAs.
+// waves per SIMD the register budget is sized for (HIP's second launch-bounds argument);
+// LDS allows the matching blocks per CU
+constexpr int sep_min_waves(int BN, int WN) { return WN == 2 ? (BN == 64 ? 3 : 2) : (BN == 128 ? 4 : 2); }
+
 template <int MODE, bool DROP, int EPI, int BN, int WN, bool WRITE_Y>
-__global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g) {
+__global__ __launch_bounds__(128 * WN, sep_min_waves(BN, WN)) void sepconv_fwd_kernel(SepArgs g) {
     constexpr int NT = 128 * WN;              // threads
     constexpr int LB = BN + 4;
     constexpr int TN = BN / (32 * WN);        // 32-column MFMA tiles per wave
@@ -47,11 +52,11 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
     constexpr int HR = (NH + NT - 1) / NT;    // per thread
     constexpr int RPT = 512 / NT;             // depthwise output rows per thread (2 or 1)
     static_assert(TN >= 1 && BQ >= 1, "tile shape");
-    constexpr int XS = HHp * HWp * LR;        // floats per halo buffer
+    constexpr int XS = HHp * HWp * XLR;       // floats of the (single) halo buffer
     // Pipeline (one barrier per k-stage): while the MFMAs consume A/B of stage kt, the same
     // waves evaluate the depthwise taps of stage kt+1 (halo already in LDS) and the global
     // loads of halo kt+2 / B kt+1 are in flight.
-    __shared__ __attribute__((aligned(16))) float Xs[2][XS];
+    __shared__ __attribute__((aligned(16))) float Xs[XS];
     __shared__ __attribute__((aligned(16))) float Ks[2][9 * BK];
     __shared__ __attribute__((aligned(16))) float As[2][128 * LR];
     __shared__ __attribute__((aligned(16))) float Bs[2][BK * LB];
@@ -70,7 +75,6 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
     const int Cin = g.Cin, C = g.x.C;
 
     float4 rb[BQ];
-    float4 rt;
     const int bq_k = tid / NQ, bq_n = tid % NQ;  // n-contiguous B: k-row, n-quad
     // Halo geometry is fixed per thread across k-stages: element e = tid + 256 j is pixel e/4 of
     // the 10x18 halo and channel quad e%4 = tid%4 of the stage.  lp = logical pixel index (-1 if
@@ -92,19 +96,22 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
         else
             sp[j] = ok ? lp[j] : 0;
     }
-    float4 rx[HR][NP];   // raw halo values in flight
-    float4 rsc, rsh;     // BN affine of this thread's channel quad
-    int hc = 0;          // channel of this thread's quad for the staged k0
-    bool hbn = false;
-    auto load_halo = [&](int k0) {
+    struct HaloRegs {
+        float4 x[HR][NP];  // raw halo values in flight
+        float4 sc, sh;     // BN affine of this thread's channel quad
+        float4 t;          // depthwise taps (threads < 36)
+        int c;             // channel of this thread's quad for the staged k0
+        bool bn;
+    };
+    auto load_halo = [&](HaloRegs& R, int k0) {
         const int c = k0 + 4 * hq;
-        hc = c;
+        R.c = c;
         const bool cok = c < Cin;
         const float* src = g.x.src0;
         int cs = g.x.c0, ci = cok ? c : 0;
         const float* scp = g.x.sc0;
         const float* shp = g.x.sh0;
-        hbn = MODE == UNET_VIEW_BNRELU || MODE == UNET_VIEW_POOL_BNRELU;
+        bool hbn = MODE == UNET_VIEW_BNRELU || MODE == UNET_VIEW_POOL_BNRELU;
         if constexpr (MODE == UNET_VIEW_CONCAT) {
             if (ci >= g.x.c0) {
                 src = g.x.src1;
@@ -115,53 +122,56 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
                 hbn = true;
             }
         }
+        R.bn = hbn;
         if constexpr (MODE != UNET_VIEW_PLAIN) {
-            rsc = hbn ? ld4(scp + ci) : f4(1.f);
-            rsh = hbn ? ld4(shp + ci) : f4(0.f);
+            R.sc = hbn ? ld4(scp + ci) : f4(1.f);
+            R.sh = hbn ? ld4(shp + ci) : f4(0.f);
         }
 #pragma unroll
         for (int j = 0; j < HR; ++j) {
             const float* b = src + (sp[j] * cs + ci);
-            rx[j][0] = ld4(b);
+            R.x[j][0] = ld4(b);
             if constexpr (NP == 4) {
                 const int rs = 2 * g.W * cs;
-                rx[j][1] = ld4(b + cs);
-                rx[j][2] = ld4(b + rs);
-                rx[j][3] = ld4(b + rs + cs);
+                R.x[j][1] = ld4(b + cs);
+                R.x[j][2] = ld4(b + rs);
+                R.x[j][3] = ld4(b + rs + cs);
             }
         }
         // depthwise taps of the stage: 9 x BK floats = 36 float4, tap-major
         const int tq = tid < 9 * (BK / 4) ? tid : 0;
         const int tp = tq / (BK / 4), c2 = k0 + 4 * (tq % (BK / 4));
-        rt = ld4(g.dk + tp * Cin + (c2 < Cin ? c2 : 0));
+        R.t = ld4(g.dk + tp * Cin + (c2 < Cin ? c2 : 0));
     };
-    auto store_halo = [&](int buf) {
+    auto store_halo = [&](const HaloRegs& R, int buf) {
+        const int hc = R.c;
         const bool cok = hc < Cin;
 #pragma unroll
         for (int j = 0; j < HR; ++j) {
             const int e = tid + NT * j;
-            float4 v = rx[j][0];
+            float4 v = R.x[j][0];
             if constexpr (NP == 4) {
-                v = fma4(v, rsc, rsh);
-                v = max4(v, fma4(rx[j][1], rsc, rsh));
-                v = max4(v, fma4(rx[j][2], rsc, rsh));
-                v = max4(v, fma4(rx[j][3], rsc, rsh));
+                v = fma4(v, R.sc, R.sh);
+                v = max4(v, fma4(R.x[j][1], R.sc, R.sh));
+                v = max4(v, fma4(R.x[j][2], R.sc, R.sh));
+                v = max4(v, fma4(R.x[j][3], R.sc, R.sh));
                 v = relu4(v);
             } else if constexpr (MODE != UNET_VIEW_PLAIN) {
-                if (hbn) v = bnrelu4(v, rsc, rsh);
+                if (R.bn) v = bnrelu4(v, R.sc, R.sh);
             }
             if constexpr (DROP) {
                 const uint64_t i = (uint64_t)(lp[j] < 0 ? 0 : lp[j]) * C + hc;
                 v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
             }
             if (lp[j] < 0 || !cok) v = f4(0.f);
-            if (e < NH) *reinterpret_cast<float4*>(&Xs[buf][(e >> 2) * LR + 4 * (e & 3)]) = v;
+            if (e < NH) *reinterpret_cast<float4*>(&Xs[4 * e]) = v;
         }
         if (tid < 9 * (BK / 4)) {
             const int c2 = hc - 4 * hq + 4 * (tid % (BK / 4));  // k0 + quad of this tap slot
-            *reinterpret_cast<float4*>(&Ks[buf][4 * tid]) = c2 < Cin ? rt : f4(0.f);
+            *reinterpret_cast<float4*>(&Ks[buf][4 * tid]) = c2 < Cin ? R.t : f4(0.f);
         }
     };
+    HaloRegs hr;
     bool bok[BQ];
     auto load_b = [&](int k0) {
 #pragma unroll
@@ -182,7 +192,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
     const int dc = (tid >> 2) & 15, dr = RPT * (tid >> 6);
     float4 ya[RPT];  // depthwise outputs of the last dw_stage (stored to y at the end of the iteration)
     auto dw_stage = [&](int buf) {
-        const float* X = Xs[buf];
+        const float* X = Xs;
         const float* Kt = Ks[buf];
         float4 a[RPT];
 #pragma unroll
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
         for (int i = 0; i < RPT + 2; ++i)
 #pragma unroll
             for (int jj = 0; jj < 3; ++jj) {
-                const float4 xv = *reinterpret_cast<const float4*>(&X[((dr + i) * HWp + dc + jj) * LR + 4 * dq]);
+                const float4 xv = *reinterpret_cast<const float4*>(&X[((dr + i) * HWp + dc + jj) * XLR + 4 * dq]);
 #pragma unroll
                 for (int o = 0; o < RPT; ++o)
                     if (i - o >= 0 && i - o < 3)
@@ -247,24 +257,32 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void sepconv_fwd_kernel(SepArgs g
     // Loads past the last stage are issued from clamped (valid) addresses and their LDS images
     // are never read, so the loop body is branch-free and the compiler's vmcnt counting stays
     // exact (a conditional load forces a full drain at the join).
-    load_halo(0);
-    load_b(0);
-    store_halo(0);
-    store_b(0);
-    load_halo(BK);
-    store_halo(1);
-    __syncthreads();
-    dw_stage(0);
-    store_y(0);
+    // Single halo buffer: dw_stage(kt+1) reads it mid-iteration, the halo of stage kt+2 is
+    // written after a barrier that follows those reads (two barriers per k-stage, one LDS copy
+    // of the halo -> three blocks per CU).
+    {
+        HaloRegs h1;  // the first two halo stages are in flight together
+        load_halo(hr, 0);
+        load_b(0);
+        load_halo(h1, BK);
+        store_halo(hr, 0);
+        store_b(0);
+        __syncthreads();
+        dw_stage(0);
+        store_y(0);
+        __syncthreads();
+        store_halo(h1, 1);
+    }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        load_halo((kt + 2) * BK);
+        load_halo(hr, (kt + 2) * BK);
         load_b((kt + 1) * BK);
         mfma_kg(buf, 0);
         dw_stage(buf ^ 1);
+        __syncthreads();  // every wave is done reading the halo of stage kt+1
         mfma_kg(buf, 1);
-        store_halo(buf);  // halo kt was consumed by dw_stage in iteration kt-1
+        store_halo(hr, buf);
         store_b(buf ^ 1);
         if (kt + 1 < nk) store_y((kt + 1) * BK);
         __syncthreads();
