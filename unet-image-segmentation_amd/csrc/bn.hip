@@ -119,9 +119,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
         if constexpr (VEC) {
             const int c = cq * 4;
             const float4 s4 = ld4(sc + c), h4 = ld4(sh + c), mu = ld4(mean + c), rs = ld4(rstd + c);
-            for (int64_t m = r0 + pl; m < r1; m += PL) {
-                const float4 zz = ld4(z + m * C + c);
-                float4 g = ld4(da + m * C + c);
+            auto accum = [&](int64_t m, float4 zz, float4 g) {
                 if constexpr (DROP) {
                     const uint64_t i = (uint64_t)m * C + c;
                     g = mul4(g, drop_mult4(seed, i, rate, inv_keep));
@@ -131,10 +129,22 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                 g.z = fmaf(zz.z, s4.z, h4.z) > 0.f ? g.z : 0.f;
                 g.w = fmaf(zz.w, s4.w, h4.w) > 0.f ? g.w : 0.f;
                 sg = add4(sg, g);
-                float4 xh = make_float4((zz.x - mu.x) * rs.x, (zz.y - mu.y) * rs.y, (zz.z - mu.z) * rs.z,
-                                        (zz.w - mu.w) * rs.w);
+                const float4 xh = make_float4((zz.x - mu.x) * rs.x, (zz.y - mu.y) * rs.y, (zz.z - mu.z) * rs.z,
+                                              (zz.w - mu.w) * rs.w);
                 sgx = fma4(g, xh, sgx);
+            };
+            int64_t m = r0 + pl;
+            for (; m + 3 * PL < r1; m += 4 * PL) {  // 8 loads in flight per thread
+                float4 zz[4], dd[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    zz[u] = ld4(z + (m + u * PL) * C + c);
+                    dd[u] = ld4(da + (m + u * PL) * C + c);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) accum(m + u * PL, zz[u], dd[u]);
             }
+            for (; m < r1; m += PL) accum(m, ld4(z + m * C + c), ld4(da + m * C + c));
         } else {
             const int c = cq;
             const float s1 = sc[c], h1 = sh[c], mu = mean[c], rs = rstd[c];

@@ -34,26 +34,82 @@ struct Geom {
     static constexpr int NE = HHp * HWp * QT;
 };
 
-// halo tile rows h0-1..h0+TH, cols w0-1..w0+TW, channels [cbase, cbase + 4 QT), zero outside
+// halo tile rows h0-1..h0+TH, cols w0-1..w0+TW, channels [cbase, cbase + 4 QT), zero outside.
+// All loads of the tile are issued first (clamped, branch-free addresses), then transformed and
+// stored, so the compiler does not wait on each load before issuing the next.
 template <int MODE, bool DROP, int QT>
 __device__ __forceinline__ void stage(float4* T, const DView& v, int n, int h0, int w0, int H, int W, int cbase) {
     using G = Geom<QT>;
-    for (int e = threadIdx.x; e < G::NE; e += 256) {
-        const int q = e % QT;
-        const int pix = e / QT;
-        const int r = pix / G::HWp;
-        const int cc = pix - r * G::HWp;
-        const int hh = h0 - 1 + r, ww = w0 - 1 + cc;
-        float4 val = f4(0.f);
-        if (hh >= 0 && hh < H && ww >= 0 && ww < W) {
-            const int c = cbase + 4 * q;
-            val = view_load4<MODE>(v, n, hh, ww, H, W, c);
-            if constexpr (DROP) {
-                const uint64_t i = ((uint64_t)((n * H + hh) * W + ww)) * v.C + c;
-                val = mul4(val, drop_mult4(v.seed, i, v.rate, v.inv_keep));
+    constexpr int NR = (G::NE + 255) / 256;
+    constexpr int NP = MODE == UNET_VIEW_POOL_BNRELU ? 4 : 1;
+    const int q = threadIdx.x % QT;  // 256 % QT == 0: the channel quad is fixed per thread
+    const int c = cbase + 4 * q;
+    // CONCAT: [raw upsample | bnrelu(skip)]; the selection is by value (no indexing into v)
+    const bool second = MODE == UNET_VIEW_CONCAT && c >= v.c0;
+    const float* src = second ? v.src1 : v.src0;
+    const int cs = second ? v.c1 : v.c0;
+    const int ci = second ? c - v.c0 : c;
+    const bool bn = MODE == UNET_VIEW_BNRELU || MODE == UNET_VIEW_POOL_BNRELU || second;
+    const float* scp = second ? v.sc1 : v.sc0;
+    const float* shp = second ? v.sh1 : v.sh0;
+    float4 sc = f4(1.f), sh = f4(0.f);
+    if constexpr (MODE != UNET_VIEW_PLAIN) {
+        if (bn) {
+            sc = ld4(scp + ci);
+            sh = ld4(shp + ci);
+        }
+    }
+    // Loads of a batch of KB elements are issued back to back, then each element is transformed,
+    // masked and written to LDS.  Non-pool views take the whole tile as one batch; the pool view
+    // reads 4 sources per element and uses batches of 3 (12 loads in flight) to bound registers.
+    constexpr int KB = NP == 4 ? 3 : NR;
+#pragma unroll
+    for (int k0 = 0; k0 < NR; k0 += KB) {
+        float4 pr[KB][NP];
+        int lp[KB];
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {
+            const int e = threadIdx.x + 256 * (k0 + kk);
+            const int pix = e / QT;
+            const int r = pix / G::HWp;
+            const int cc = pix - r * G::HWp;
+            const int hh = h0 - 1 + r, ww = w0 - 1 + cc;
+            const bool ok = k0 + kk < NR && e < G::NE && hh >= 0 && hh < H && ww >= 0 && ww < W;
+            lp[kk] = ok ? (n * H + hh) * W + ww : -1;
+            int sp = 0;
+            if (ok) {
+                if constexpr (MODE == UNET_VIEW_POOL_BNRELU) sp = (n * 2 * H + 2 * hh) * (2 * W) + 2 * ww;
+                else sp = lp[kk];
+            }
+            const float* b = src + ((int64_t)sp * cs + ci);
+            pr[kk][0] = ld4(b);
+            if constexpr (NP == 4) {
+                const int64_t rs = (int64_t)2 * W * cs;
+                pr[kk][1] = ld4(b + cs);
+                pr[kk][2] = ld4(b + rs);
+                pr[kk][3] = ld4(b + rs + cs);
             }
         }
-        T[e] = val;
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {
+            const int e = threadIdx.x + 256 * (k0 + kk);
+            float4 val = pr[kk][0];
+            if constexpr (NP == 4) {
+                val = fma4(val, sc, sh);
+                val = max4(val, fma4(pr[kk][1], sc, sh));
+                val = max4(val, fma4(pr[kk][2], sc, sh));
+                val = max4(val, fma4(pr[kk][3], sc, sh));
+                val = relu4(val);
+            } else if constexpr (MODE != UNET_VIEW_PLAIN) {
+                if (bn) val = bnrelu4(val, sc, sh);
+            }
+            if constexpr (DROP) {
+                const uint64_t i = (uint64_t)(lp[kk] < 0 ? 0 : lp[kk]) * v.C + c;
+                val = mul4(val, drop_mult4(v.seed, i, v.rate, v.inv_keep));
+            }
+            if (lp[kk] < 0) val = f4(0.f);
+            if (k0 + kk < NR && e < G::NE) T[e] = val;
+        }
     }
 }
 
@@ -67,7 +123,7 @@ __device__ __forceinline__ void tile_coords(int b, int tiles_w, int tiles_h, int
 }
 
 template <int MODE, bool DROP, int QT>
-__global__ __launch_bounds__(256) void dw_tile_fwd(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+__global__ __launch_bounds__(256, 3) void dw_tile_fwd(DView v, int N, int H, int W, int tiles_w, int tiles_h,
                                                    const float* __restrict__ K, float* __restrict__ Y) {
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
@@ -106,7 +162,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd(DView v, int N, int H, int W,
 }
 
 template <int MODE, bool DROP, int QT>
-__global__ __launch_bounds__(256) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+__global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
                                                         const float* __restrict__ K, const float* __restrict__ dY,
                                                         float* __restrict__ dx0, float* __restrict__ dx1) {
     using G = Geom<QT>;
@@ -195,7 +251,7 @@ __global__ __launch_bounds__(256) void dw_tile_bwd_data(DView v, int N, int H, i
 }
 
 template <int MODE, bool DROP, int QT>
-__global__ __launch_bounds__(256) void dw_tile_bwd_filter(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+__global__ __launch_bounds__(256, 2) void dw_tile_bwd_filter(DView v, int N, int H, int W, int tiles_w, int tiles_h,
                                                           int ntiles, const float* __restrict__ dY,
                                                           float* __restrict__ part) {
     using G = Geom<QT>;
@@ -210,10 +266,18 @@ __global__ __launch_bounds__(256) void dw_tile_bwd_filter(DView v, int N, int H,
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         int n, h0, w0;
         tile_coords(tile, tiles_w, tiles_h, G::TW, n, h0, w0);
+        const int w = w0 + col;
+        // the tile's 8 dy rows: issued with the halo loads (clamped addresses, masked on use)
+        float4 gy[TH];
+        const bool wok = w < W;
+#pragma unroll
+        for (int r = 0; r < TH; ++r) {
+            const bool ok = wok && h0 + r < H;
+            gy[r] = ld4(dY + (ok ? ((int64_t)(n * H + h0 + r) * W + w) * C + c : 0));
+        }
         __syncthreads();  // previous tile's readers are done with T
         stage<MODE, DROP, QT>(T, v, n, h0, w0, H, W, cbase);
         __syncthreads();
-        const int w = w0 + col;
         float4 a[3][3];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -223,8 +287,7 @@ __global__ __launch_bounds__(256) void dw_tile_bwd_filter(DView v, int N, int H,
         for (int r = 0; r < TH; ++r) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
-            const int h = h0 + r;
-            const float4 g = (w < W && h < H) ? ld4(dY + ((int64_t)(n * H + h) * W + w) * C + c) : f4(0.f);
+            const float4 g = (wok && h0 + r < H) ? gy[r] : f4(0.f);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
