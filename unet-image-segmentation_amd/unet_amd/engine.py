@@ -50,9 +50,10 @@ class Block:
     """One conv_block (SeparableConv2D -> BatchNormalization -> ReLU)."""
 
     name: str
-    cin: int
+    cin: int    # channels the kernels see (the image block is padded to a multiple of 4)
     cout: int
     level: int  # spatial size = input / 2**level
+    wcin: int = 0  # channels of the Keras weights when they differ from cin (padded block)
 
 
 @dataclass
@@ -81,6 +82,7 @@ class Acts:
     dy: torch.Tensor
     sums: torch.Tensor
     result: torch.Tensor
+    xpad: Optional[torch.Tensor] = None  # channel-padded image (image block input)
 
 
 class UNetEngine:
@@ -157,8 +159,13 @@ class UNetEngine:
         f = self.filters
         self.enc: List[tuple] = []
         c = self.c
+        # The image block runs on a channel-padded copy of the input (3 -> 4 channels, zero
+        # padding), so every kernel takes its vectorised / fused path; its Keras-shaped weights
+        # are mirrored into padded buffers each forward and the gradients copied back.
+        self.cpad = c if c % 4 == 0 else (c + 3) // 4 * 4
         for i, fi in enumerate(f):
-            b1 = Block(f"enc{i + 1}_block1", c, fi, i)
+            b1 = Block(f"enc{i + 1}_block1", c, fi, i) if i > 0 or self.cpad == c else \
+                Block(f"enc{i + 1}_block1", self.cpad, fi, i, wcin=c)
             b2 = Block(f"enc{i + 1}_block2", fi, fi, i)
             self.enc.append((f"enc{i + 1}", b1, b2))
             c = fi
@@ -226,8 +233,7 @@ class UNetEngine:
         m = n * h * w
         bb = A.blocks[b.name]
         gamma, beta, mm, mv = self._bn(b.name)
-        dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
-        pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
+        dk, pk = self._wts(b)
         fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= 64 * 64)
         if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight grad
@@ -242,13 +248,52 @@ class UNetEngine:
             return View.bnrelu(bb.z, bb.scale, bb.shift)
         ops.dwconv3x3_fwd(view, n, h, w, dk, bb.y)
         if training and self.use_bn:
-            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, self.vars[f"{b.name}_sepconv/pointwise_kernel"], bb.z, bb.part)
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, bb.part)
             ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
                             bb.scale, bb.shift)
         else:
-            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, self.vars[f"{b.name}_sepconv/pointwise_kernel"], bb.z, None)
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, None)
             ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
         return View.bnrelu(bb.z, bb.scale, bb.shift)
+
+    def _wts(self, b: Block):
+        """(depthwise, pointwise) kernels of a block as the kernels see them."""
+        dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
+        pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
+        if not b.wcin:
+            return dk, pk
+        pad = self._pad_w
+        pad["dk"][:, :, :b.wcin].copy_(dk)
+        pad["pk"][:, :, :b.wcin].copy_(pk)
+        return pad["dk"], pad["pk"]
+
+    def _gwts(self, b: Block):
+        """(depthwise, pointwise) gradient buffers the kernels write for a block."""
+        if not b.wcin:
+            return self.gvars[f"{b.name}_sepconv/depthwise_kernel"], self.gvars[f"{b.name}_sepconv/pointwise_kernel"]
+        return self._pad_w["gdk"], self._pad_w["gpk"]
+
+    @property
+    def _pad_w(self):
+        p = getattr(self, "_pad_w_bufs", None)
+        if p is None:
+            b = self.blocks[0]
+            z = dict(dtype=torch.float32, device=self.device)
+            p = {"dk": torch.zeros((3, 3, b.cin, 1), **z), "pk": torch.zeros((1, 1, b.cin, b.cout), **z),
+                 "gdk": torch.zeros((3, 3, b.cin, 1), **z), "gpk": torch.zeros((1, 1, b.cin, b.cout), **z)}
+            self._pad_w_bufs = p
+        return p
+
+    def _padded_input(self, A: Acts, x: torch.Tensor) -> torch.Tensor:
+        """The image with its channels zero-padded to self.cpad (a persistent buffer per batch)."""
+        if self.cpad == self.c:
+            return x
+        xp = getattr(A, "xpad", None)
+        if xp is None or xp.shape[0] != x.shape[0]:
+            xp = torch.zeros((x.shape[0], self.h, self.w, self.cpad), dtype=torch.float32, device=self.device)
+            A.xpad = xp
+        xp[..., :self.c].copy_(x)
+        return xp
 
     def drop_seeds(self, step: int) -> Dict[str, int]:
         return {s: _mix64(self.seed, step, i + 1) for i, s in enumerate(DROP_SITES)}
@@ -264,6 +309,8 @@ class UNetEngine:
         drop = training and self.dropout_rate > 0.0
         if drop and seeds is None:
             seeds = self.drop_seeds(self.step_count + 1)
+        x = self._padded_input(A, x)
+        self._x_fwd = x
         v = View.plain(x)
         for stage, b1, b2 in self.enc:
             v = self._block_fwd(A, b1, v, training)
@@ -322,8 +369,7 @@ class UNetEngine:
             dgamma, dbeta = self.gvars[f"{b.name}_bn/gamma"], self.gvars[f"{b.name}_bn/beta"]
         else:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
-        pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
-        dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
+        dk, pk = self._wts(b)
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
             ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
@@ -334,16 +380,21 @@ class UNetEngine:
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
-        gpk = self.gvars[f"{b.name}_sepconv/pointwise_kernel"]
-        gdk = self.gvars[f"{b.name}_sepconv/depthwise_kernel"]
+        gdk, gpk = self._gwts(b)
+
+        def weight_grads():
+            ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
+            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+            if b.wcin:  # padded image block: keep the Keras-shaped slices
+                self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
+                self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
+
         if self.overlap:  # weight gradients off the critical path, on the side stream
             self.side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.side):
-                ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-                ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+                weight_grads()
         else:
-            ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+            weight_grads()
         if dx0 is not None:
             ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
@@ -407,7 +458,7 @@ class UNetEngine:
         seeds = self.drop_seeds(self.step_count) if self.dropout_rate > 0 else None
         x = x.contiguous()
         self.forward(x, training=True, seeds=seeds)
-        self._x_last = x
+        self._x_last = self._x_fwd
         self._acts_last = self.acts(x.shape[0])
         return self.loss(y_true.contiguous(), x.shape[0])
 
