@@ -82,12 +82,16 @@ def encoder_block_roofline(batch, size, device, reps=10):
             src = torch.rand((batch, 2 * hh if pool else hh, 2 * hh if pool else hh, ci), generator=g).to(device)
             sc = torch.rand(ci, generator=g).to(device) + 0.5
             sh = torch.randn(ci, generator=g).to(device) * 0.1
+            ck = ci
+            if lvl == 0 and blk == 0 and ci % 4:  # the engine zero-pads the image to 4 channels
+                ck = (ci + 3) // 4 * 4
+                src = torch.cat([src, torch.zeros(src.shape[:3] + (ck - ci,), device=device)], dim=3)
             view = View.plain(src) if (lvl == 0 and blk == 0) else (View.pool_bnrelu(src, sc, sh) if pool
                                                                      else View.bnrelu(src, sc, sh))
-            dk = torch.randn((3, 3, ci, 1), generator=g).to(device)
-            pk = (torch.randn((1, 1, ci, co), generator=g) / ci ** 0.5).to(device)
+            dk = torch.randn((3, 3, ck, 1), generator=g).to(device)
+            pk = (torch.randn((1, 1, ck, co), generator=g) / ci ** 0.5).to(device)
             m = batch * hh * hh
-            ybuf = torch.empty((batch, hh, hh, ci), device=device)
+            ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
             part = torch.empty(ops.bn_partials_numel(m, co), device=device)
             fused = ops.sepconv_supported(view, batch, hh, hh, co)
@@ -97,7 +101,7 @@ def encoder_block_roofline(batch, size, device, reps=10):
                     ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf, z, part)
                 else:
                     ops.dwconv3x3_fwd(view, batch, hh, hh, dk, ybuf)
-                    ops.pointwise_fwd(ybuf, m, ci, co, pk, z, part)
+                    ops.pointwise_fwd(ybuf, m, ck, co, pk, z, part)
             for _ in range(3):
                 run()
             ts = []
@@ -113,7 +117,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
             nb = 4.0 * (m * (ci + co) + 9 * ci + ci * co + 4 * co)
             t_roof = max(fl / (PEAK_FP32_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)) * 1e6
             rows.append({"block": f"enc{lvl + 1}_block{blk + 1}", "hw": hh, "cin": ci, "cout": co,
-                         "kernel": "unet_sepconv_fwd" if fused else "dwconv3x3_fwd+pointwise_fwd",
+                         "kernel": ("unet_sepconv_fwd" if fused else "dwconv3x3_fwd+pointwise_fwd") +
+                                   (f" (input padded {ci}->{ck} ch)" if ck != ci else ""),
                          "bound": "mfma" if fl / nb >= RIDGE else "hbm", "us": round(us, 1),
                          "t_roof_us": round(t_roof, 1), "frac": round(t_roof / us, 4),
                          "tflops": round(fl / us / 1e6, 1)})
@@ -131,7 +136,7 @@ def pmc_traffic(op):
     """HBM bytes per launch of `op` from the newest committed PMC summary (profiles/*_traffic.json,
     written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench)."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):

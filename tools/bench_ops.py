@@ -57,6 +57,7 @@ for mode, h, w, c0, c1, cout in SHAPES:
     y = torch.empty(N, h, w, C, device="cuda")
     z = torch.empty(N, h, w, cout, device="cuda")
     dz = torch.randn(N, h, w, cout, device="cuda")
+    dz2 = torch.empty(N, h, w, cout, device="cuda")
     dy = torch.randn(N, h, w, C, device="cuda")
     part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
     ddk = torch.empty(3, 3, C, 1, device="cuda")
@@ -71,6 +72,11 @@ for mode, h, w, c0, c1, cout in SHAPES:
         dx0 = torch.empty(N, h, w, c0, device="cuda")
         dx1 = torch.empty(N, h, w, c1, device="cuda") if mode == 3 else None
         report(tag, "dw_bwd_data", timeit(lambda: ops.dwconv3x3_bwd_data(v, N, h, w, dk, dy, dx0, dx1)), 2 * act)
+    coef = torch.randn(3 * cout, device="cuda") * 0.01
+    scl2, shf2 = torch.rand(cout, device="cuda") + 0.5, torch.randn(cout, device="cuda") * 0.1
+    report(tag, "pw_dgrad_bn", timeit(lambda: ops.pointwise_bwd_data_bnrelu(dz, z, m, C, cout, pk, scl2, shf2, coef, 0.0,
+                                                                         0, dy, dz2)),
+           4.0 * (2 * m * cout + m * C + m * cout), gf)
     g = torch.rand(cout, device="cuda") + 0.5
     b = torch.randn(cout, device="cuda")
     mu, rs, scl, shf = (torch.rand(cout, device="cuda") for _ in range(4))
@@ -78,5 +84,5 @@ for mode, h, w, c0, c1, cout in SHAPES:
     dzz = torch.empty_like(z)
     report(tag, "bn_relu_bwd", timeit(lambda: ops.bn_relu_bwd(dz, z, m, cout, mu, rs, scl, shf, True, 0.0, 0, dg, db,
                                                                dzz)), 3 * m * cout * 4)
-    del src, s1, y, z, dz, dy, dzz
+    del src, s1, y, z, dz, dy, dzz, dz2
     torch.cuda.empty_cache()

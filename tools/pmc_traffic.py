@@ -19,6 +19,7 @@ OPS = {
     "unet_pointwise_bwd_data": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 0, (true|false)>|gemm_rows_kernel<\d+, \d+, 0, false, 0>",
     "unet_pointwise_bwd_filter": r"gemm_wgrad_(vec|kernel)<\d+, \d+, 0, false, 0, false>",
     "unet_sepconv_fwd": r"sepconv_fwd_kernel<",
+    "unet_pointwise_bwd_data_bnrelu": r"gemm_rows_vec<\d+, \d+, \d+, 3, (true|false), 0, (true|false)>",
 }
 
 
