@@ -130,8 +130,10 @@ int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_ke
  * batch mean / variance, writes mean, rstd = 1/sqrt(var+eps), and the affine
  * scale = gamma*rstd, shift = beta - mean*scale consumed by views; updates
  * moving stats when update_moving != 0.  gamma == NULL means
- * use_batch_norm=False: scale = 1, shift = beta (the sepconv bias).        */
-int unet_bn_finalize(const float* bn_partials, int64_t m, int c,
+ * use_batch_norm=False: scale = 1, shift = beta (the sepconv bias).
+ * The tail of bn_partials (past the per-tile partials) is scratch for the
+ * two-pass reduction: the buffer must hold unet_bn_partials_size bytes.     */
+int unet_bn_finalize(float* bn_partials, int64_t m, int c,
                      const float* gamma, const float* beta, float eps,
                      float momentum, float* moving_mean, float* moving_var,
                      int update_moving, float* mean, float* rstd,

@@ -39,7 +39,8 @@ def test_view_struct_layout_matches_c():
 def test_workspace_queries():
     from unet_amd import _lib
     q = _lib.query
-    assert q("unet_bn_partials_size", 1000, 64) == 8 * 64 * 8  # ceil(1000/128) tiles x C x float2
+    # ceil(1000/128) tiles x C x float2 (256-B aligned) + one chunk record x C x double2 of finalize scratch
+    assert q("unet_bn_partials_size", 1000, 64) == 8 * 64 * 8 + 1 * 64 * 16
     assert q("unet_bn_partials_size", 0, 64) == 0
     for fn, args in [("unet_dwconv3x3_bwd_filter_workspace", (16, 256, 256, 64)),
                      ("unet_pointwise_bwd_filter_workspace", (16 * 65536, 64, 64)),

@@ -119,11 +119,13 @@ def test_dwconv_bwd(ops, mode, n, h, w, c0, c1, drop):
         assert rel_err(host(dx0), ref) < 2e-6
 
 
-@pytest.mark.parametrize("m,cin,cout", [(100, 3, 64), (256, 64, 64), (300, 64, 128), (128, 128, 256),
-                                        (77, 32, 96), (512, 256, 512)])
-def test_pointwise_and_bn_stats(ops, m, cin, cout):
+@pytest.mark.parametrize("m,cin,cout,off", [(100, 3, 64, 0.0), (256, 64, 64, 0.0), (300, 64, 128, 0.0),
+                                            (128, 128, 256, 0.0), (77, 32, 96, 0.0), (512, 256, 512, 0.0),
+                                            # > 64 partials: several finalize chunks; |mean| >> std
+                                            (24653, 64, 64, 0.0), (24653, 32, 128, 25.0)])
+def test_pointwise_and_bn_stats(ops, m, cin, cout, off):
     rng = np.random.default_rng(m + cin)
-    y = f32(rng.standard_normal((m, cin)))
+    y = f32(rng.standard_normal((m, cin)) + off)
     pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cin))
     z = torch.empty((m, cout), device="cuda")
     part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")

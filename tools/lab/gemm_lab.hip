@@ -1,0 +1,78 @@
+// Timing lab for the rows GEMM (pointwise fwd / BN-backward dgrad shapes of the U-Net at
+// batch 16, 256x256).  Includes the product gemm.hip so its kernels can be instantiated with
+// other tile parameters; candidate kernels are added below.  Prints us and TF/s per variant,
+// and max |diff| against the product kernel's output.
+#include "gemm.hip"
+#include <vector>
+#include <cmath>
+#include <cstdlib>
+
+using namespace unet;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+static float* dalloc(size_t n, float scale, unsigned seed) {
+    std::vector<float> h(n);
+    srand(seed);
+    for (size_t i = 0; i < n; ++i) h[i] = scale * ((float)rand() / RAND_MAX * 2.f - 1.f);
+    float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    return d;
+}
+static double maxdiff(const float* a, const float* b, size_t n) {
+    std::vector<float> x(n), y(n);
+    CK(hipMemcpy(x.data(), a, n * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(y.data(), b, n * 4, hipMemcpyDeviceToHost));
+    double m = 0, r = 0;
+    for (size_t i = 0; i < n; ++i) { m = fmax(m, fabs((double)x[i] - y[i])); r = fmax(r, fabs((double)y[i])); }
+    return m / (r + 1e-30);
+}
+
+template <class F> static double timeit(F f, int it = 20) {
+    for (int i = 0; i < 3; ++i) f();
+    hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    CK(hipEventRecord(a)); for (int i = 0; i < it; ++i) f(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipGetLastError());
+    return ms * 1e3 / it;
+}
+
+#include "gemm_lab_variants.inc"
+
+int main(int argc, char** argv) {
+    struct Shape { int64_t M; int K, N; int mode; };  // mode 0: fwd (B [K][N]), 1: dgrad BN-bwd (B [N][K])
+    std::vector<Shape> shapes = {
+        {1048576, 64, 64, 0}, {262144, 128, 128, 0}, {65536, 256, 256, 0}, {16384, 512, 512, 0}, {4096, 1024, 1024, 0},
+        {16384, 1024, 512, 0}, {16384, 4096, 512, 0}, {65536, 2048, 256, 0},
+        {1048576, 64, 64, 1}, {1048576, 64, 128, 1}, {262144, 128, 128, 1}, {262144, 128, 256, 1}, {65536, 256, 256, 1},
+        {16384, 512, 512, 1}, {16384, 512, 1024, 1}, {4096, 1024, 1024, 1},
+    };
+    const char* only = getenv("LAB_SHAPE");
+    int si = -1;
+    for (auto& s : shapes) {
+        ++si;
+        if (only && atoi(only) != si) continue;
+        const int64_t M = s.M; const int K = s.K, N = s.N;
+        float* A = dalloc(M * K, 1.f, 1);
+        float* Z = dalloc(M * K, 1.f, 2);
+        float* B = dalloc((size_t)K * N, 0.1f, 3);
+        float* C0; CK(hipMalloc(&C0, M * N * 4));
+        float* C1; CK(hipMalloc(&C1, M * N * 4));
+        float* side; CK(hipMalloc(&side, M * K * 4));
+        float2* stats; CK(hipMalloc(&stats, (M / 32 + 1) * N * 8));
+        float* sc = dalloc(K, 1.f, 4); float* sh = dalloc(K, 0.5f, 5); float* coef = dalloc(3 * K, 0.1f, 6);
+        RowsArgs a{};
+        unet_view v{}; v.mode = UNET_VIEW_PLAIN; v.c0 = K; v.src0 = A;
+        a.a = make_dview(v);
+        a.M = M; a.K = K; a.N = N; a.B = B; a.ldc = N;
+        if (s.mode == 0) { a.sbk = N; a.sbn = 1; a.stats = stats; }
+        else { a.sbk = 1; a.sbn = K; a.a.sc0 = sc; a.a.sh0 = sh; a.a.rate = 0.2f; a.a.inv_keep = 1.25f; a.a.seed = 77;
+               a.z = Z; a.coef = coef; a.side = side; }
+        const double fl = 2.0 * M * K * N;
+        printf("M=%ld K=%d N=%d %s\n", (long)M, K, N, s.mode == 0 ? "fwd+stats" : "dgrad_bnbwd+drop");
+        run_variants(s.mode, a, C0, C1, fl, M * N);
+        CK(hipFree(A)); CK(hipFree(Z)); CK(hipFree(B)); CK(hipFree(C0)); CK(hipFree(C1)); CK(hipFree(side));
+        CK(hipFree(stats)); CK(hipFree(sc)); CK(hipFree(sh)); CK(hipFree(coef));
+        fflush(stdout);
+    }
+    return 0;
+}

@@ -14,53 +14,77 @@ namespace unet {
 namespace {
 constexpr int kStatsRows = 128;
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int64_t nblk, int64_t M,
-                                                          int C, const float* __restrict__ gamma,
+// Pass 1: per (chunk of kChunkParts partials, channel) sums of the moments shifted by
+// K_c = mean of partial 0 (no cancellation when |mean| >> std):  S1 = sum n_b (mean_b - K),
+// S2 = sum M2_b + n_b (mean_b - K)^2, in double, fixed order (4 lanes, then lane order).
+// Coalesced: consecutive threads read consecutive channels of one partial row.
+constexpr int kChunkParts = 64;
+__global__ __launch_bounds__(256) void bn_stats_chunk_kernel(const float2* __restrict__ part, int64_t nblk, int64_t M,
+                                                             int C, double2* __restrict__ chunks) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int lane = threadIdx.x >> 6;
+    const int64_t b0 = (int64_t)blockIdx.y * kChunkParts;
+    const int64_t b1 = b0 + kChunkParts < nblk ? b0 + kChunkParts : nblk;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+        const double K = (double)part[c].x;
+#pragma unroll 4
+        for (int64_t b = b0 + lane; b < b1; b += 4) {
+            const float2 pm = part[b * C + c];
+            const int64_t rows = (M - b * kStatsRows) < kStatsRows ? (M - b * kStatsRows) : kStatsRows;
+            const double d = (double)pm.x - K;
+            const double nd = (double)rows * d;
+            s1 += nd;
+            s2 += (double)pm.y + nd * d;
+        }
+    }
+    __shared__ double r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    if (lane == 0 && c < C) {
+        for (int l = 1; l < 4; ++l) {
+            s1 += r1[threadIdx.x + 64 * l];
+            s2 += r2[threadIdx.x + 64 * l];
+        }
+        chunks[(int64_t)blockIdx.y * C + c] = make_double2(s1, s2);
+    }
+}
+
+// Pass 2: per channel, chunk sums in chunk order -> mean, biased var, folded affine, moving update.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const double2* __restrict__ chunks, int nch,
+                                                          const float2* __restrict__ part, int64_t M, int C,
+                                                          const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, float momentum,
                                                           float* moving_mean, float* moving_var, int update_moving,
                                                           float* mean_out, float* rstd_out, float* scale_out,
                                                           float* shift_out) {
-    const int c = blockIdx.x;
-    const int t = threadIdx.x;
-    Moments acc{0.0, 0.0, 0.0};
-    for (int64_t b = t; b < nblk; b += 256) {
-        const float2 pm = part[b * C + c];
-        const int64_t rows = (M - b * kStatsRows) < kStatsRows ? (M - b * kStatsRows) : kStatsRows;
-        acc = moments_combine(acc, Moments{(double)rows, (double)pm.x, (double)pm.y});
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < nch; ++k) {
+        const double2 v = chunks[(int64_t)k * C + c];
+        s1 += v.x;
+        s2 += v.y;
     }
-    __shared__ double sn[256], smean[256], sm2[256];
-    sn[t] = acc.n;
-    smean[t] = acc.mean;
-    sm2[t] = acc.m2;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (t < s) {
-            Moments a{sn[t], smean[t], sm2[t]}, b{sn[t + s], smean[t + s], sm2[t + s]};
-            Moments r = moments_combine(a, b);
-            sn[t] = r.n;
-            smean[t] = r.mean;
-            sm2[t] = r.m2;
-        }
-        __syncthreads();
+    const double dm = s1 / (double)M;
+    const float mean = (float)((double)part[c].x + dm);
+    double vd = s2 / (double)M - dm * dm;
+    const float var = (float)(vd > 0.0 ? vd : 0.0);
+    const float rstd = 1.0f / sqrtf(var + eps);
+    if (gamma) {
+        const float sc = gamma[c] * rstd;
+        scale_out[c] = sc;
+        shift_out[c] = beta[c] - mean * sc;
+    } else {  // use_batch_norm=False: relu(z + bias)
+        scale_out[c] = 1.0f;
+        shift_out[c] = beta ? beta[c] : 0.f;
     }
-    if (t == 0) {
-        const float mean = (float)smean[0];
-        const float var = (float)(sm2[0] / (double)M);
-        const float rstd = 1.0f / sqrtf(var + eps);
-        if (gamma) {
-            const float sc = gamma[c] * rstd;
-            scale_out[c] = sc;
-            shift_out[c] = beta[c] - mean * sc;
-        } else {  // use_batch_norm=False: relu(z + bias)
-            scale_out[c] = 1.0f;
-            shift_out[c] = beta ? beta[c] : 0.f;
-        }
-        if (mean_out) mean_out[c] = mean;
-        if (rstd_out) rstd_out[c] = rstd;
-        if (update_moving && moving_mean && moving_var) {
-            moving_mean[c] = moving_mean[c] * momentum + mean * (1.0f - momentum);
-            moving_var[c] = moving_var[c] * momentum + var * (1.0f - momentum);
-        }
+    if (mean_out) mean_out[c] = mean;
+    if (rstd_out) rstd_out[c] = rstd;
+    if (update_moving && moving_mean && moving_var) {
+        moving_mean[c] = moving_mean[c] * momentum + mean * (1.0f - momentum);
+        moving_var[c] = moving_var[c] * momentum + var * (1.0f - momentum);
     }
 }
 
@@ -288,6 +312,7 @@ int grid_for(int64_t work) {
 }
 }  // namespace
 
+size_t bn_partials_bytes(int64_t m, int c);
 size_t colsum_workspace(int64_t rows, int cols) {
     RedPlan p = red_plan(rows, cols);
     return align_up((size_t)p.chunks * cols * sizeof(float), 256);
@@ -311,15 +336,28 @@ int colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t 
 
 using namespace unet;
 
-extern "C" int unet_bn_finalize(const float* bn_partials, int64_t m, int c, const float* gamma, const float* beta,
+size_t unet::bn_partials_bytes(int64_t m, int c) {
+    const int64_t nblk = cdiv(m, kStatsRows);
+    return align_up((size_t)nblk * c * sizeof(float2), 256) +
+           (size_t)cdiv(nblk, kChunkParts) * c * sizeof(double2);
+}
+
+extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const float* gamma, const float* beta,
                                 float eps, float momentum, float* moving_mean, float* moving_var, int update_moving,
                                 float* mean, float* rstd, float* scale, float* shift, unet_stream_t stream) {
     UNET_CHECK_ARG(bn_partials && scale && shift && m > 0 && c > 0, "unet_bn_finalize: bad args");
     UNET_CHECK_ARG(!gamma || beta, "unet_bn_finalize: gamma without beta");
-    bn_finalize_kernel<<<c, 256, 0, as_stream(stream)>>>(reinterpret_cast<const float2*>(bn_partials),
-                                                         cdiv(m, kStatsRows), m, c, gamma, beta, eps, momentum,
-                                                         moving_mean, moving_var, update_moving, mean, rstd, scale,
-                                                         shift);
+    hipStream_t st = as_stream(stream);
+    const int64_t nblk = cdiv(m, kStatsRows);
+    const int nch = (int)cdiv(nblk, kChunkParts);
+    const float2* part = reinterpret_cast<const float2*>(bn_partials);
+    double2* chunks = reinterpret_cast<double2*>(reinterpret_cast<char*>(bn_partials) +
+                                                 align_up((size_t)nblk * c * sizeof(float2), 256));
+    bn_stats_chunk_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, st>>>(part, nblk, m, c, chunks);
+    UNET_CHECK_LAUNCH("unet_bn_finalize(chunks)");
+    bn_finalize_kernel<<<(unsigned)cdiv(c, 256), 256, 0, st>>>(chunks, nch, part, m, c, gamma, beta, eps, momentum,
+                                                               moving_mean, moving_var, update_moving, mean, rstd,
+                                                               scale, shift);
     UNET_CHECK_LAUNCH("unet_bn_finalize");
     return 0;
 }

@@ -22,6 +22,7 @@
 namespace unet {
 
 int colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, hipStream_t st);
+size_t bn_partials_bytes(int64_t m, int c);
 size_t colsum_workspace(int64_t rows, int cols);
 
 namespace {
@@ -602,23 +603,33 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         __syncthreads();
     }
 
+    const bool full = M_rem == BM;  // every row of the tile exists: no per-row checks
     if constexpr (EPI == E_STORE || EPI == E_STATS) {
+        const int ldc = (int)g.ldc;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
                 if (n >= g.N) continue;
+                const int rb0 = wm * (BM / 2) + tm * 32 + 4 * hi;  // acc_row(r, hi) = rb0 + acc_row(r, 0)
+                float* cp = g.C + (int64_t)(m0 + rb0) * g.ldc + n;
+                if (full) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
-                    if (rr < M_rem) g.C[(int64_t)(m0 + rr) * g.ldc + n] = acc[tm][tn][r];
+                    for (int r = 0; r < 16; ++r) cp[acc_row(r, 0) * ldc] = acc[tm][tn][r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (rb0 + acc_row(r, 0) < M_rem) cp[acc_row(r, 0) * ldc] = acc[tm][tn][r];
                 }
             }
     }
     if constexpr (EPI == E_STATS) {
-        float* red = &As[0][0];
-        float mean[TN];
+        // Per-wave (mean, M2) over its BM/2 rows, then one Chan combine of the two row-halves
+        // (one barrier); the partial is the (mean, M2) of the tile's M_rem rows.
+        float2* red = reinterpret_cast<float2*>(&As[0][0]);
+        const int wr0 = wm * (BM / 2);
+        const int cnt = M_rem - wr0 < 0 ? 0 : (M_rem - wr0 < BM / 2 ? M_rem - wr0 : BM / 2);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
             const int col = wn * (BN / 2) + tn * 32 + lo;
@@ -627,39 +638,38 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) s += acc[tm][tn][r];
+                    if (full || wr0 + tm * 32 + acc_row(r, hi) < M_rem) s += acc[tm][tn][r];
             s += __shfl_xor(s, 32, 64);
-            if (hi == 0) red[wm * BN + col] = s;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-            const int col = wn * (BN / 2) + tn * 32 + lo;
-            mean[tn] = (red[col] + red[BN + col]) / (float)M_rem;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-            const int col = wn * (BN / 2) + tn * 32 + lo;
+            const float mean = cnt > 0 ? s / (float)cnt : 0.f;
             float q = 0.f;
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    if (wm * (BM / 2) + tm * 32 + acc_row(r, hi) < M_rem) {
-                        const float d = acc[tm][tn][r] - mean[tn];
+                    if (full || wr0 + tm * 32 + acc_row(r, hi) < M_rem) {
+                        const float d = acc[tm][tn][r] - mean;
                         q = fmaf(d, d, q);
                     }
             q += __shfl_xor(q, 32, 64);
-            if (hi == 0) red[wm * BN + col] = q;
+            if (hi == 0) red[wm * BN + col] = make_float2(mean, q);
         }
         __syncthreads();
         if (wm == 0 && hi == 0) {
+            const float na = (float)(M_rem < BM / 2 ? M_rem : BM / 2);
+            const float nb = (float)M_rem - na;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int col = wn * (BN / 2) + tn * 32 + lo;
                 const int n = n0 + col;
-                if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = make_float2(mean[tn], red[col] + red[BN + col]);
+                const float2 a = red[col], b = red[BN + col];
+                float2 o = a;
+                if (nb > 0.f) {
+                    const float d = b.x - a.x;
+                    const float f = nb / (float)M_rem;
+                    o.x = a.x + d * f;
+                    o.y = a.y + b.y + d * d * na * f;
+                }
+                if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = o;
             }
         }
     }
@@ -845,48 +855,63 @@ bool rows_vec_ok(const RowsArgs& a, int amode) {
     return ((uintptr_t)a.a.src0 | (uintptr_t)a.B) % 16 == 0;
 }
 
+// Tile configuration of the vectorised rows GEMM: BN columns x BK k per stage (BM = 128).
+// Chosen per operand mode from lab timings (tools/lab/gemm_lab.hip) on the U-Net shapes:
+// the BatchNorm-backward data gradient forms its A operand per N-tile, so it prefers the
+// 256-wide tile when the grid still fills the chip, and BK = 32 otherwise; plain operands
+// take BK = 32 from K = 256 on.  UNET_ROWS_CFG="BN,BK" overrides (tuning only).
+struct RowsCfg {
+    int bn, bk;
+};
+RowsCfg rows_cfg(const RowsArgs& a, int amode) {
+    static int env_bn = -1, env_bk = 0;
+    if (env_bn < 0) {
+        env_bn = 0;
+        if (const char* e = getenv("UNET_ROWS_CFG")) sscanf(e, "%d,%d", &env_bn, &env_bk);
+    }
+    if (env_bn > 0) return RowsCfg{env_bn, env_bk};
+    if (amode == A_BNBWD) {
+        if (a.N <= 64) return RowsCfg{64, 32};
+        if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
+        return RowsCfg{128, 32};
+    }
+    if (a.N <= 64) return RowsCfg{64, 16};
+    return RowsCfg{128, a.K >= 256 ? 32 : 16};
+}
+
+template <int BN, int BKk, int AMODE, bool DROP, int EPI>
+void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
+    dim3 grid((unsigned)cdiv(a.M, 128), (unsigned)cdiv(a.N, BN));
+    if (a.sbk == 1) gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
+    else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
+}
+
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
-    const unsigned gm = (unsigned)cdiv(a.M, 128);
-    if constexpr (AMODE == A_BNBWD) {  // vectorised kernel only
-        UNET_CHECK_ARG(rows_vec_ok(a, AMODE), "%s: needs channel counts divisible by 4 and 16-B aligned operands",
-                       what);
-        if (a.N <= 64) {
-            dim3 grid(gm, (unsigned)cdiv(a.N, 64));
-            if (a.sbk == 1) gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
-            else gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
-        } else {
-            dim3 grid(gm, (unsigned)cdiv(a.N, 128));
-            if (a.sbk == 1) gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
-            else gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
-        }
-        UNET_CHECK_LAUNCH(what);
-        return 0;
-    } else {
     if (rows_vec_ok(a, AMODE)) {
-        const bool bkc = a.sbk == 1;
-        if (a.N <= 64) {
-            dim3 grid(gm, (unsigned)cdiv(a.N, 64));
-            if (bkc) gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
-            else gemm_rows_vec<128, 64, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
-        } else {
-            dim3 grid(gm, (unsigned)cdiv(a.N, 128));
-            if (bkc) gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
-            else gemm_rows_vec<128, 128, 16, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
-        }
+        const RowsCfg c = rows_cfg(a, AMODE);
+        if (c.bn == 64 && c.bk == 16) launch_rows_tile<64, 16, AMODE, DROP, EPI>(a, st);
+        else if (c.bn == 64 && c.bk == 32) launch_rows_tile<64, 32, AMODE, DROP, EPI>(a, st);
+        else if (c.bn == 128 && c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI>(a, st);
+        else if (c.bn == 256 && c.bk == 16) launch_rows_tile<256, 16, AMODE, DROP, EPI>(a, st);
+        else launch_rows_tile<128, 16, AMODE, DROP, EPI>(a, st);
         UNET_CHECK_LAUNCH(what);
         return 0;
     }
-    if (a.N <= 64) {
-        dim3 grid(gm, (unsigned)cdiv(a.N, 64));
-        gemm_rows_kernel<128, 64, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+    if constexpr (AMODE == A_BNBWD) {  // vectorised kernel only
+        UNET_CHECK_ARG(false, "%s: needs channel counts divisible by 4 and 16-B aligned operands", what);
     } else {
-        dim3 grid(gm, (unsigned)cdiv(a.N, 128));
-        gemm_rows_kernel<128, 128, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+        const unsigned gm = (unsigned)cdiv(a.M, 128);
+        if (a.N <= 64) {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 64));
+            gemm_rows_kernel<128, 64, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+        } else {
+            dim3 grid(gm, (unsigned)cdiv(a.N, 128));
+            gemm_rows_kernel<128, 128, AMODE, DROP, EPI><<<grid, 256, 0, st>>>(a);
+        }
+        UNET_CHECK_LAUNCH(what);
     }
-    UNET_CHECK_LAUNCH(what);
     return 0;
-    }
 }
 
 struct WgradPlan {
@@ -991,7 +1016,7 @@ using namespace unet;
 // ------------------------------------------------------------------- pointwise conv ----
 extern "C" size_t unet_bn_partials_size(int64_t m, int c) {
     if (m <= 0 || c <= 0) return 0;
-    return (size_t)cdiv(m, kStatsRows) * c * sizeof(float2);
+    return bn_partials_bytes(m, c);  // partials + the finalize's chunk scratch (bn.hip)
 }
 
 extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, const float* pw_kernel, float* z,
