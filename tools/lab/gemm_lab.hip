@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
     struct Shape { int64_t M; int K, N; int mode; };  // mode 0: fwd (B [K][N]), 1: dgrad BN-bwd (B [N][K])
     std::vector<Shape> shapes = {
         {1048576, 64, 64, 0}, {262144, 128, 128, 0}, {65536, 256, 256, 0}, {16384, 512, 512, 0}, {4096, 1024, 1024, 0},
-        {16384, 1024, 512, 0}, {16384, 4096, 512, 0}, {65536, 2048, 256, 0},
+        {16384, 1024, 512, 0}, {16384, 4096, 512, 0}, {65536, 2048, 256, 0}, {8192, 4096, 512, 0}, {32768, 4096, 512, 0},
         {1048576, 64, 64, 1}, {1048576, 64, 128, 1}, {262144, 128, 128, 1}, {262144, 128, 256, 1}, {65536, 256, 256, 1},
         {16384, 512, 512, 1}, {16384, 512, 1024, 1}, {4096, 1024, 1024, 1},
     };

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void bn_stats_chunk_kernel(const float2* __res
     }
 }
 
-// Pass 2: per channel, chunk sums in chunk order -> mean, biased var, folded affine, moving update.
+// Pass 2: per channel, chunk sums (4 lanes over interleaved chunks, combined in lane order)
+// -> mean, biased var, folded affine, moving update.  64 channels per block.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double2* __restrict__ chunks, int nch,
                                                           const float2* __restrict__ part, int64_t M, int C,
                                                           const float* __restrict__ gamma,
@@ -59,13 +60,25 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double2* __restr
                                                           float* moving_mean, float* moving_var, int update_moving,
                                                           float* mean_out, float* rstd_out, float* scale_out,
                                                           float* shift_out) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int lane = threadIdx.x >> 6;
     double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < nch; ++k) {
-        const double2 v = chunks[(int64_t)k * C + c];
-        s1 += v.x;
-        s2 += v.y;
+    if (c < C) {
+#pragma unroll 8
+        for (int k = lane; k < nch; k += 4) {
+            const double2 v = chunks[(int64_t)k * C + c];
+            s1 += v.x;
+            s2 += v.y;
+        }
+    }
+    __shared__ double r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    if (lane != 0 || c >= C) return;
+    for (int l = 1; l < 4; ++l) {
+        s1 += r1[threadIdx.x + 64 * l];
+        s2 += r2[threadIdx.x + 64 * l];
     }
     const double dm = s1 / (double)M;
     const float mean = (float)((double)part[c].x + dm);
@@ -114,7 +127,7 @@ RedPlan red_plan(int64_t rows, int cols) {
     const int CQ = cols % 4 == 0 ? cols / 4 : cols;
     p.CT = CQ < 64 ? CQ : 64;
     p.ctiles = (int)cdiv(CQ, p.CT);
-    int64_t want = cdiv(2048, p.ctiles);
+    int64_t want = cdiv(1024, p.ctiles);
     int64_t maxc = cdiv(rows, 128);
     p.chunks = want < maxc ? want : maxc;
     if (p.chunks < 1) p.chunks = 1;
@@ -273,6 +286,49 @@ __global__ void bn_bwd_coef_kernel(const float* sums, int C, int64_t M, int use_
     coef[2 * C + c] = use_bn ? rstd[c] * (s2 * invM) : 0.f;
 }
 
+// Statistics-only finish: the fixed-order slab reduction of (S1, S2) fused with the coefficient
+// kernel above.  Block = 16 channel quads x 32 slab groups; group g sums slabs g, g+32, ... in
+// double, then a fixed-order tree over the groups (same order as reduce_tall4).
+__global__ __launch_bounds__(512) void bn_bwd_finish_kernel(const float* __restrict__ part, int S, int C, int64_t M,
+                                                            int use_bn, const float* mean, const float* rstd,
+                                                            float* dgamma, float* dbeta, float* coef) {
+    constexpr int LQ = 16, G = 32;
+    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
+    const int c = (blockIdx.x * LQ + q) * 4;
+    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (c < C) {
+        for (int s = g; s < S; s += G) {
+            const float4 u = ld4(part + (int64_t)s * 2 * C + c);
+            const float4 v = ld4(part + (int64_t)s * 2 * C + C + c);
+            a[0] += (double)u.x; a[1] += (double)u.y; a[2] += (double)u.z; a[3] += (double)u.w;
+            a[4] += (double)v.x; a[5] += (double)v.y; a[6] += (double)v.z; a[7] += (double)v.w;
+        }
+    }
+    __shared__ double red[8][G * LQ];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = a[k];
+    __syncthreads();
+    for (int half = G / 2; half > 0; half >>= 1) {
+        if (g < half) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + half * LQ];
+        }
+        __syncthreads();
+    }
+    if (g != 0 || c >= C) return;
+    const float invM = 1.0f / (float)M;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int cc = c + k;
+        const float s1 = (float)red[k][q], s2 = (float)red[4 + k][q];
+        if (dbeta) dbeta[cc] = s1;
+        if (use_bn && dgamma) dgamma[cc] = s2;
+        coef[cc] = use_bn ? mean[cc] : 0.f;
+        coef[C + cc] = use_bn ? s1 * invM : 0.f;
+        coef[2 * C + cc] = use_bn ? rstd[cc] * (s2 * invM) : 0.f;
+    }
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, int64_t rows, int C, int CT,
                                                      int64_t rpc, float* __restrict__ part) {
@@ -355,7 +411,7 @@ extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const floa
                                                  align_up((size_t)nblk * c * sizeof(float2), 256));
     bn_stats_chunk_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, st>>>(part, nblk, m, c, chunks);
     UNET_CHECK_LAUNCH("unet_bn_finalize(chunks)");
-    bn_finalize_kernel<<<(unsigned)cdiv(c, 256), 256, 0, st>>>(chunks, nch, part, m, c, gamma, beta, eps, momentum,
+    bn_finalize_kernel<<<(unsigned)cdiv(c, 64), 256, 0, st>>>(chunks, nch, part, m, c, gamma, beta, eps, momentum,
                                                                moving_mean, moving_var, update_moving, mean, rstd,
                                                                scale, shift);
     UNET_CHECK_LAUNCH("unet_bn_finalize");
@@ -412,6 +468,12 @@ int bn_relu_bwd_impl(const float* da, const float* z, int64_t m, int c, const fl
     }
 #undef UNET_BNB
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(reduce)");
+    if (coef_out && vec) {  // statistics-only entry (unet_bn_relu_bwd_stats): reduce + coefficients
+        bn_bwd_finish_kernel<<<(unsigned)cdiv(c / 4, 16), 512, 0, st>>>(part, (int)p.chunks, c, m, use_bn, mean, rstd,
+                                                                        dgamma, dbeta, coef_out);
+        UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats(finish)");
+        return 0;
+    }
     int rc = reduce_slabs(part, (int)p.chunks, (int64_t)2 * c, sums, (int64_t)2 * c, (int64_t)2 * c, st);
     if (rc) return rc;
     if (coef_out) {  // statistics-only entry (unet_bn_relu_bwd_stats): no dz pass

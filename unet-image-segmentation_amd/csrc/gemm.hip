@@ -876,7 +876,7 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
         return RowsCfg{128, 32};
     }
     if (a.N <= 64) return RowsCfg{64, 16};
-    return RowsCfg{128, a.K >= 256 ? 32 : 16};
+    return RowsCfg{128, a.K >= 256 && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
 template <int BN, int BKk, int AMODE, bool DROP, int EPI>

@@ -128,7 +128,13 @@ class UNetEngine:
         self.grad_hook: Optional[Callable[[int], None]] = None  # called with a flat-offset low-water mark
         # Off-critical-path backward work (weight gradients of the pointwise and depthwise
         # convolutions) runs on a second HIP stream, overlapping the data-gradient chain.
-        self.side = torch.cuda.Stream(device=self.device)
+        # The critical path runs on a high-priority stream (model.train_step enters it) so the
+        # dispatcher hands freed CU slots to its workgroups before the side stream's; the side
+        # stream's weight-gradient grids otherwise hold slots the data-gradient chain waits for.
+        lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+        prio = os.environ.get("UNET_PRIO", "1") != "0"
+        self.main = torch.cuda.Stream(device=self.device, priority=hi_prio if prio else 0)
+        self.side = torch.cuda.Stream(device=self.device, priority=lo_prio if prio else 0)
         self.overlap = os.environ.get("UNET_OVERLAP", "1") != "0"  # 0: single stream (clean profiles)
         # Fused depthwise+pointwise forward (unet_sepconv_fwd) vs the two launches: "auto" uses it
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and

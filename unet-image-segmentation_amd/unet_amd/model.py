@@ -82,15 +82,20 @@ class UNetModel:
             self.compile()
         x = as_device_tensor(x, self.engine.device)
         y = as_device_tensor(y, self.engine.device)
-        res = self.engine.forward_train(x, y)
-        if self.mean_iou is not None:
-            self.mean_iou.update_state(y, self.engine.acts(x.shape[0]).prob)
-        if self.loss_kind == L.LOSS_IOU:
-            res = res.clone()
-            res[0] = 1.0 - res[2]
-        self.engine.backward(y, self.loss_kind)
-        scale = self.bucketer.finish() if self.bucketer is not None else 1.0
-        self.optimizer.apply(self.engine.params, self.engine.grads, scale)
+        caller = torch.cuda.current_stream(self.engine.device)
+        main = self.engine.main
+        main.wait_stream(caller)
+        with torch.cuda.stream(main):
+            res = self.engine.forward_train(x, y)
+            if self.mean_iou is not None:
+                self.mean_iou.update_state(y, self.engine.acts(x.shape[0]).prob)
+            if self.loss_kind == L.LOSS_IOU:
+                res = res.clone()
+                res[0] = 1.0 - res[2]
+            self.engine.backward(y, self.loss_kind)
+            scale = self.bucketer.finish() if self.bucketer is not None else 1.0
+            self.optimizer.apply(self.engine.params, self.engine.grads, scale)
+        caller.wait_stream(main)
         return res
 
     def test_step(self, x, y) -> torch.Tensor:
