@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 1
+#define UNET_ABI_VERSION 2
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -90,6 +90,21 @@ int unet_dwconv3x3_fwd(const unet_view* x, int n, int h, int w,
 int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w,
                             const float* dw_kernel, const float* dy,
                             float* dx0, float* dx1, unet_stream_t stream);
+/* POOL_BNRELU view only (the MaxPooling2D of u_net.py:69 feeding the next
+ * encoder block): unet_dwconv3x3_bwd_data plus the BatchNorm-backward partial
+ * sums of the pooled block, whose da this launch completes (it adds the pooled
+ * half of the gradient to the stored skip half and reads the block's raw z for
+ * the argmax anyway): bn_partials[s][0][c] = sum g, [s][1][c] = sum g*xhat over
+ * slab s, g = da*[z*scale+shift > 0], xhat = (z-mean)*rstd (mean/rstd NULL when
+ * use_batch_norm=False).  Replaces unet_bn_relu_bwd_stats's pass over (da, z);
+ * finish with unet_bn_relu_bwd_stats_finish.  _slabs returns the slab count S
+ * (bn_partials holds S*2*C floats), 0 if the shape has no such path.          */
+int unet_dwconv3x3_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w);
+int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w,
+                                    const float* dw_kernel, const float* dy,
+                                    float* dx0, const float* mean,
+                                    const float* rstd, float* bn_partials,
+                                    unet_stream_t stream);
 
 size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c);
 /* d_dw_kernel (3,3,C,1) = sum over pixels of x(shifted) * dy (overwrites). */
@@ -165,6 +180,12 @@ int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c,
                            float drop_rate, uint64_t drop_seed, float* dgamma,
                            float* dbeta, float* coef, void* ws, size_t ws_bytes,
                            unet_stream_t stream);
+/* Finish of the statistics from S producer-side partial slabs ([S][2][c],
+ * fixed-order double reduction): the outputs of unet_bn_relu_bwd_stats.     */
+int unet_bn_relu_bwd_stats_finish(const float* partials, int S, int64_t m, int c,
+                                  const float* mean, const float* rstd,
+                                  int use_bn, float* dgamma, float* dbeta,
+                                  float* coef, unet_stream_t stream);
 /* Pointwise data gradient of a conv_block whose output went through BN + ReLU
  * (+ dropout): dz = scale*(g - coef_p - (z - coef_mu)*coef_q),
  * g = da * keep/(1-rate) * [z*scale+shift > 0], is formed while loading the GEMM

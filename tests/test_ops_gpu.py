@@ -394,3 +394,47 @@ def test_fused_sepconv_unsupported_shapes(ops):
     assert not ops.sepconv_supported(ops.View.plain(x), 1, 8, 8, 64)     # w % 16 != 0
     x3 = torch.zeros((1, 16, 16, 3), device="cuda")
     assert not ops.sepconv_supported(ops.View.plain(x3), 1, 16, 16, 64)  # 3 channels
+
+
+@pytest.mark.parametrize("use_bn", [True, False])
+@pytest.mark.parametrize("n,h,w,c", [(2, 8, 16, 64), (2, 5, 7, 16), (1, 4, 4, 128), (3, 8, 8, 8)])
+def test_dwconv_bwd_data_pool_bnstats(ops, use_bn, n, h, w, c):
+    """Pool-view data gradient that also emits the pooled block's BN-backward partials: dx0
+    bitwise equal to the plain launch, statistics equal to unet_bn_relu_bwd_stats's."""
+    rng = np.random.default_rng(n * 100 + h * 10 + c)
+    a, t = _view_inputs(rng, 2, n, h, w, c)
+    v = _mk_view(ops, 2, t)
+    dk = dev(f32(rng.standard_normal((3, 3, c, 1))))
+    dy = dev(f32(rng.standard_normal((n, h, w, c))))
+    init = f32(rng.standard_normal((n, 2 * h, 2 * w, c)))
+    S = ops.dwconv3x3_bwd_data_bnstats_slabs(v, n, h, w)
+    assert S > 0
+    mean = dev(f32(rng.standard_normal(c) * 0.1))
+    rstd = dev(f32(1.0 + rng.random(c)))
+    part = torch.empty(S * 2 * c, device="cuda")
+    dx_f, dx_p = dev(init), dev(init)
+    ops.dwconv3x3_bwd_data_bnstats(v, n, h, w, dk, dy, dx_f, mean if use_bn else None, rstd if use_bn else None,
+                                   part)
+    ops.dwconv3x3_bwd_data(v, n, h, w, dk, dy, dx_p)
+    assert torch.equal(dx_f, dx_p)
+    m = n * 4 * h * w
+    outs = []
+    for fused in (True, False):
+        dg, db, coef = (torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"),
+                        torch.empty(3 * c, device="cuda"))
+        if fused:
+            ops.bn_relu_bwd_stats_finish(part, S, m, c, mean, rstd, use_bn, dg if use_bn else None, db, coef)
+        else:
+            ops.bn_relu_bwd_stats(dx_p, t["src0"], m, c, mean, rstd, t["sc0"], t["sh0"], use_bn, 0.0, 0,
+                                  dg if use_bn else None, db, coef)
+        outs.append((host(dg), host(db), host(coef)))
+    for x, y in zip(outs[0], outs[1]):
+        assert rel_err(x, y) < 2e-5
+    # and against float64 numpy: g = da * [z*sc+sh > 0], dbeta = sum g, dgamma = sum g*xhat
+    da = host(dx_p).astype(np.float64).reshape(-1, c)
+    z = a["src0"].astype(np.float64).reshape(-1, c)
+    g = np.where(z * a["sc0"] + a["sh0"] > 0, da, 0.0)
+    assert rel_err(outs[0][1], g.sum(0)) < 1e-5
+    if use_bn:
+        xh = (z - host(mean)) * host(rstd)
+        assert rel_err(outs[0][0], (g * xh).sum(0)) < 1e-5

@@ -511,6 +511,18 @@ extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int 
                             nullptr, ws, ws_bytes, stream);
 }
 
+extern "C" int unet_bn_relu_bwd_stats_finish(const float* partials, int S, int64_t m, int c, const float* mean,
+                                             const float* rstd, int use_bn, float* dgamma, float* dbeta, float* coef,
+                                             unet_stream_t stream) {
+    UNET_CHECK_ARG(partials && coef && S > 0 && m > 0 && c > 0, "unet_bn_relu_bwd_stats_finish: bad args");
+    UNET_CHECK_ARG(c % 4 == 0, "unet_bn_relu_bwd_stats_finish: channels must be a multiple of 4");
+    UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_relu_bwd_stats_finish: use_bn needs mean/rstd");
+    bn_bwd_finish_kernel<<<(unsigned)cdiv(c / 4, 16), 512, 0, as_stream(stream)>>>(partials, S, c, m, use_bn, mean,
+                                                                                   rstd, dgamma, dbeta, coef);
+    UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats_finish");
+    return 0;
+}
+
 extern "C" int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c, const float* mean,
                                       const float* rstd, const float* scale, const float* shift, int use_bn,
                                       float drop_rate, uint64_t drop_seed, float* dgamma, float* dbeta, float* coef,

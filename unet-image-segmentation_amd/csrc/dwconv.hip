@@ -381,6 +381,9 @@ size_t dw_tiled_filter_partials(int N, int H, int W, int C);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
 bool dw_tiled_ok(int C);
+int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
+                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st);
+size_t dw_tiled_ntiles(int N, int H, int W, int C);
 
 static int check_dims(const unet_view* x, int n, int h, int w, const char* op) {
     UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "%s: bad shape n=%d h=%d w=%d", op, n, h, w);
@@ -439,6 +442,26 @@ extern "C" int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w, 
     UNET_DW_DISPATCH(dw_bwd_data_kernel, grid, v, n, h, w, dw_kernel, dy, dx0, dx1);
     UNET_CHECK_LAUNCH("unet_dwconv3x3_bwd_data");
     return 0;
+}
+
+extern "C" int unet_dwconv3x3_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w) {
+    if (!x || x->mode != UNET_VIEW_POOL_BNRELU || n <= 0 || h <= 0 || w <= 0) return 0;
+    if (!view_vec(x) || !dw_tiled_ok(x->c0)) return 0;
+    return (int)dw_tiled_ntiles(n, h, w, x->c0);
+}
+
+extern "C" int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                                               const float* dy, float* dx0, const float* mean, const float* rstd,
+                                               float* bn_partials, unet_stream_t stream) {
+    const char* op = "unet_dwconv3x3_bwd_data_bnstats";
+    if (check_view(x, op) || check_dims(x, n, h, w, op)) return -1;
+    UNET_CHECK_ARG(dw_kernel && dy && dx0 && bn_partials, "%s: null pointer", op);
+    UNET_CHECK_ARG(unet_dwconv3x3_bwd_data_bnstats_slabs(x, n, h, w) > 0,
+                   "%s: needs a POOL_BNRELU view with channels %% 4 == 0 (tiled path)", op);
+    UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "%s: mean and rstd go together", op);
+    const DView v = make_dview(*x);
+    return dw_tiled_bwd_data_bnstats(v, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
+                                     as_stream(stream));
 }
 
 extern "C" size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c) {

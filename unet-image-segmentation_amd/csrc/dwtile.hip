@@ -18,6 +18,9 @@ int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const
 int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
                       float* dx0, float* dx1, hipStream_t st);
 size_t dw_tiled_filter_partials(int N, int H, int W, int C);
+int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
+                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st);
+size_t dw_tiled_ntiles(int N, int H, int W, int C);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
 bool dw_tiled_ok(int C);
@@ -161,10 +164,18 @@ __global__ __launch_bounds__(256, 3) void dw_tile_fwd(DView v, int N, int H, int
     }
 }
 
-template <int MODE, bool DROP, int QT>
+// STATS (POOL view only): this kernel is the last writer of the pooled block's da (it adds the
+// pooled half to the stored skip half) and reads that block's raw z for the argmax, so it also
+// emits the block's BatchNorm-backward partial sums over its tile: bnpart[tile][0][c] = sum g,
+// bnpart[tile][1][c] = sum g * xhat with g = da * [z*sc+sh > 0], xhat = (z - mu) * rs (the
+// unet_bn_relu_bwd_stats reduction, without its separate pass over (da, z)).
+template <int MODE, bool DROP, int QT, bool STATS = false>
 __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
                                                         const float* __restrict__ K, const float* __restrict__ dY,
-                                                        float* __restrict__ dx0, float* __restrict__ dx1) {
+                                                        float* __restrict__ dx0, float* __restrict__ dx1,
+                                                        const float* __restrict__ mu = nullptr,
+                                                        const float* __restrict__ rs = nullptr,
+                                                        float* __restrict__ bnpart = nullptr) {
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
     int n, h0, w0;
@@ -183,6 +194,14 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
     for (int t = 0; t < 9; ++t) kf[t] = ld4(K + (8 - t) * C + c);
     __syncthreads();
     const int w = w0 + col;
+    float4 s1 = f4(0.f), s2 = f4(0.f);  // STATS partial sums of this thread's pixels
+    float4 smu = f4(0.f), srs = f4(0.f);
+    if constexpr (STATS) {
+        if (mu) {
+            smu = ld4(mu + c);
+            srs = ld4(rs + c);
+        }
+    }
     float4 a[3][3];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -221,10 +240,11 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
             const int64_t b = ((int64_t)(n * 2 * H + 2 * h) * W2 + 2 * w) * v.c0 + c;
             const int64_t off[4] = {0, v.c0, (int64_t)W2 * v.c0, (int64_t)W2 * v.c0 + v.c0};
             const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
-            float4 xv[4], g[4];
+            float4 zr[4], xv[4], g[4];
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
-                xv[qq] = bnrelu4(ld4(v.src0 + b + off[qq]), sc, sh);
+                zr[qq] = ld4(v.src0 + b + off[qq]);
+                xv[qq] = bnrelu4(zr[qq], sc, sh);
                 g[qq] = ld4(dx0 + b + off[qq]);
             }
 #define UNET_ROUTE(comp)                                                   \
@@ -246,6 +266,36 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
 #undef UNET_ROUTE
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) st4(dx0 + b + off[qq], g[qq]);
+            if constexpr (STATS) {
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) {
+                    const float4 gm = make_float4(xv[qq].x > 0.f ? g[qq].x : 0.f, xv[qq].y > 0.f ? g[qq].y : 0.f,
+                                                  xv[qq].z > 0.f ? g[qq].z : 0.f, xv[qq].w > 0.f ? g[qq].w : 0.f);
+                    s1 = add4(s1, gm);
+                    const float4 xh = make_float4((zr[qq].x - smu.x) * srs.x, (zr[qq].y - smu.y) * srs.y,
+                                                  (zr[qq].z - smu.z) * srs.z, (zr[qq].w - smu.w) * srs.w);
+                    s2 = fma4(gm, xh, s2);
+                }
+            }
+        }
+    }
+    if constexpr (STATS) {  // fixed-order reduction over the TW column lanes of each channel quad
+        float* out = bnpart + (int64_t)blockIdx.x * 2 * C;
+        __syncthreads();
+        T[threadIdx.x] = s1;
+        __syncthreads();
+        if (col == 0) {
+            float4 t = T[q];
+            for (int cl = 1; cl < G::TW; ++cl) t = add4(t, T[cl * QT + q]);
+            st4(out + c, t);
+        }
+        __syncthreads();
+        T[threadIdx.x] = s2;
+        __syncthreads();
+        if (col == 0) {
+            float4 t = T[q];
+            for (int cl = 1; cl < G::TW; ++cl) t = add4(t, T[cl * QT + q]);
+            st4(out + C + c, t);
         }
     }
 }
@@ -389,6 +439,34 @@ int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, 
     UNET_CHECK_LAUNCH("dwconv3x3_bwd_data(tiled)");
     return 0;
 }
+
+int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
+                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st) {
+    TilePlan p = tile_plan(N, H, W, v.C);
+    dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
+#define UNET_BNS(D, Q)                                                                                       \
+    dw_tile_bwd_data<UNET_VIEW_POOL_BNRELU, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, K, \
+                                                                              dY, dx0, nullptr, mu, rs, bnpart)
+#define UNET_BNS_QT(D)                      \
+    switch (p.qt) {                          \
+        case 16: UNET_BNS(D, 16); break;     \
+        case 8: UNET_BNS(D, 8); break;       \
+        case 4: UNET_BNS(D, 4); break;       \
+        case 2: UNET_BNS(D, 2); break;       \
+        default: UNET_BNS(D, 1); break;      \
+    }
+    if (drop) {
+        UNET_BNS_QT(true)
+    } else {
+        UNET_BNS_QT(false)
+    }
+#undef UNET_BNS_QT
+#undef UNET_BNS
+    UNET_CHECK_LAUNCH("dwconv3x3_bwd_data_bnstats(tiled)");
+    return 0;
+}
+
+size_t dw_tiled_ntiles(int N, int H, int W, int C) { return (size_t)tile_plan(N, H, W, C).ntiles; }
 
 size_t dw_tiled_filter_partials(int N, int H, int W, int C) {
     TilePlan p = tile_plan(N, H, W, C);

@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -47,6 +47,8 @@ SIGNATURES = {
     "unet_view_materialize": (c_int, [_VP, c_int, c_int, c_int, P, P]),
     "unet_dwconv3x3_fwd": (c_int, [_VP, c_int, c_int, c_int, P, P, P]),
     "unet_dwconv3x3_bwd_data": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P]),
+    "unet_dwconv3x3_bwd_data_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int]),
+    "unet_dwconv3x3_bwd_data_bnstats": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P]),
     "unet_dwconv3x3_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
     "unet_dwconv3x3_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "unet_bn_partials_size": (c_size_t, [c_int64, c_int]),
@@ -61,6 +63,7 @@ SIGNATURES = {
     "unet_bn_relu_bwd_workspace": (c_size_t, [c_int64, c_int]),
     "unet_bn_relu_bwd": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                  c_size_t, P]),
+    "unet_bn_relu_bwd_stats_finish": (c_int, [P, c_int, c_int64, c_int, P, P, c_int, P, P, P, P]),
     "unet_bn_relu_bwd_stats": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                        c_size_t, P]),
     "unet_pointwise_bwd_data_bnrelu": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, c_float, c_uint64, P, P,

@@ -69,6 +69,8 @@ class BlockBufs:
     dz: Optional[torch.Tensor] = None  # backward-only, allocated on first backward
     dy: Optional[torch.Tensor] = None
     coef: Optional[torch.Tensor] = None  # BN-backward coefficients (mean, dbeta/M, rstd*dgamma/M)
+    bnpart: Optional[torch.Tensor] = None  # BN-backward partial sums emitted by the producer of da
+    bn_slabs: int = 0  # > 0: bnpart holds this many fresh slabs for the next backward of the block
 
 
 @dataclass
@@ -142,6 +144,9 @@ class UNetEngine:
         self.fuse_sepconv = "auto"
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
+        # BN-backward statistics of a pooled encoder block emitted by the launch that completes its
+        # da (the next block's depthwise data gradient through the max-pool), not by a pass over (da, z)
+        self.fuse_bn_stats = os.environ.get("UNET_FUSE_BN_STATS", "1") != "0"
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -361,7 +366,10 @@ class UNetEngine:
             else:
                 self.grad_hook(self.train_layout.offsets[name])
 
-    def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0):
+    def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0,
+                   pool_target: Optional[BlockBufs] = None):
+        """Backward of one conv_block.  pool_target: the encoder block whose output view_in max-pools;
+        dx0 (its da) is completed here and, on the fused path, so are its BN-backward partials."""
         n = A.n
         h, w = self._dims(b.level)
         m = n * h * w
@@ -378,8 +386,13 @@ class UNetEngine:
         dk, pk = self._wts(b)
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
-            ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
-                                  drop_rate, drop_seed, dgamma, dbeta, bb.coef)
+            if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
+                ops.bn_relu_bwd_stats_finish(bb.bnpart, bb.bn_slabs, m, b.cout, bb.mean, bb.rstd, self.use_bn,
+                                             dgamma, dbeta, bb.coef)
+            else:
+                ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
+                                      drop_rate, drop_seed, dgamma, dbeta, bb.coef)
+            bb.bn_slabs = 0
             ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef, drop_rate,
                                           drop_seed, dy, dz)
         else:
@@ -402,7 +415,19 @@ class UNetEngine:
         else:
             weight_grads()
         if dx0 is not None:
-            ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
+            S = 0
+            if pool_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
+                S = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w)
+            if S > 0:
+                tb = pool_target
+                need = S * 2 * view_in.channels
+                if tb.bnpart is None or tb.bnpart.numel() < need:
+                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                ops.dwconv3x3_bwd_data_bnstats(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
+                                               tb.rstd if self.use_bn else None, tb.bnpart)
+                tb.bn_slabs = S
+            else:
+                ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
     def _view_of(self, A: Acts, b: Block) -> View:
@@ -446,13 +471,13 @@ class UNetEngine:
                         drop_seed=seeds["bneck_dropout"] if drop else 0)
         e4 = A.blocks[self.enc[-1][2].name]
         # pooled half ACCUMULATES into the encoder block's da (the skip half is already there)
-        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da)
+        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, pool_target=e4)
         for j in reversed(range(len(self.enc))):
             stage, e1, e2 = self.enc[j]
             self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da)
             if j > 0:
                 pb = A.blocks[self.enc[j - 1][2].name]
-                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da)
+                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, pool_target=pb)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
         if self.overlap:

@@ -204,6 +204,28 @@ def dwconv3x3_bwd_data(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Tensor, dx
           _ptr(dx1), _stream())
 
 
+def dwconv3x3_bwd_data_bnstats_slabs(x: View, n, h, w) -> int:
+    """Slab count of dwconv3x3_bwd_data_bnstats's BatchNorm partials (0: no fused path)."""
+    vs = x.c_struct()
+    return L.query("unet_dwconv3x3_bwd_data_bnstats_slabs", ctypes.byref(vs), n, h, w)
+
+
+def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Tensor, mean, rstd,
+                               partials: Tensor):
+    """POOL view: dwconv3x3_bwd_data that also emits the pooled block's BN-backward partials."""
+    C = x.channels
+    S = dwconv3x3_bwd_data_bnstats_slabs(x, n, h, w)
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(dy, "dy", n * h * w * C)
+    _check(dx0, "dx0")
+    _check(partials, "bn_partials", S * 2 * C)
+    vs = x.c_struct()
+    m = n * h * w
+    nb = 8.0 * m * C + 3.0 * x.src_bytes(n, h, w) + 4.0 * S * 2 * C
+    _call("unet_dwconv3x3_bwd_data_bnstats", (18.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy),
+          _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
+
+
 def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
     C = x.channels
     _check(dy, "dy", n * h * w * C)
@@ -302,6 +324,15 @@ def bn_relu_bwd_stats(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, 
     _call("unet_bn_relu_bwd_stats", (8.0 * m * c, 8.0 * m * c), _ptr(da), _ptr(z), m, c, _ptr(mean), _ptr(rstd),
           _ptr(scale), _ptr(shift), int(bool(use_bn)), float(drop_rate), int(drop_seed) & 0xFFFFFFFFFFFFFFFF,
           _ptr(dgamma), _ptr(dbeta), _ptr(coef), ws, wsb, _stream())
+
+
+def bn_relu_bwd_stats_finish(partials: Tensor, S: int, m: int, c: int, mean, rstd, use_bn: bool, dgamma, dbeta,
+                             coef: Tensor):
+    """bn_relu_bwd_stats's outputs from producer-side partial slabs ([S][2][c])."""
+    _check(partials, "bn_partials", S * 2 * c)
+    _check(coef, "coef", 3 * c)
+    _call("unet_bn_relu_bwd_stats_finish", (2.0 * S * c, 8.0 * S * c), _ptr(partials), S, m, c, _ptr(mean),
+          _ptr(rstd), int(bool(use_bn)), _ptr(dgamma), _ptr(dbeta), _ptr(coef), _stream())
 
 
 def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
