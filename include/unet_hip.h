@@ -90,16 +90,18 @@ int unet_dwconv3x3_fwd(const unet_view* x, int n, int h, int w,
 int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w,
                             const float* dw_kernel, const float* dy,
                             float* dx0, float* dx1, unet_stream_t stream);
-/* POOL_BNRELU view only (the MaxPooling2D of u_net.py:69 feeding the next
- * encoder block): unet_dwconv3x3_bwd_data plus the BatchNorm-backward partial
- * sums of the pooled block, whose da this launch completes (it adds the pooled
- * half of the gradient to the stored skip half and reads the block's raw z for
- * the argmax anyway): bn_partials[s][0][c] = sum g, [s][1][c] = sum g*xhat over
+/* POOL_BNRELU view (the MaxPooling2D of u_net.py:69 feeding the next encoder
+ * block) or BNRELU view (block1 -> block2 of a stage): unet_dwconv3x3_bwd_data
+ * plus the BatchNorm-backward partial sums of the view's block, whose da this
+ * launch completes (POOL: adds the pooled half of the gradient to the stored
+ * skip half, reading the block's raw z for the argmax anyway; BNRELU: writes
+ * all of da and reads z once for the ReLU mask): bn_partials[s][0][c] = sum g, [s][1][c] = sum g*xhat over
  * slab s, g = da*[z*scale+shift > 0], xhat = (z-mean)*rstd (mean/rstd NULL when
  * use_batch_norm=False).  Replaces unet_bn_relu_bwd_stats's pass over (da, z);
  * finish with unet_bn_relu_bwd_stats_finish.  _slabs returns the slab count S
  * (bn_partials holds S*2*C floats), 0 if the shape has no such path.          */
 int unet_dwconv3x3_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w);
+/* (bn_partials: unet_bn_stats_partials_size(S, C) bytes, see the finish below) */
 int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w,
                                     const float* dw_kernel, const float* dy,
                                     float* dx0, const float* mean,
@@ -181,8 +183,11 @@ int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c,
                            float* dbeta, float* coef, void* ws, size_t ws_bytes,
                            unet_stream_t stream);
 /* Finish of the statistics from S producer-side partial slabs ([S][2][c],
- * fixed-order double reduction): the outputs of unet_bn_relu_bwd_stats.     */
-int unet_bn_relu_bwd_stats_finish(const float* partials, int S, int64_t m, int c,
+ * fixed-order double reduction): the outputs of unet_bn_relu_bwd_stats.  The
+ * partials buffer holds unet_bn_stats_partials_size(S, c) bytes: the slabs,
+ * then scratch for the first pass of large slab counts.                      */
+size_t unet_bn_stats_partials_size(int S, int c);
+int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, int c,
                                   const float* mean, const float* rstd,
                                   int use_bn, float* dgamma, float* dbeta,
                                   float* coef, unet_stream_t stream);
@@ -242,6 +247,17 @@ int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
                   const float* y_true, const float* sums, float smooth,
                   int loss_kind, float* dx, float* dkernel, float* dbias,
                   void* ws, size_t ws_bytes, unet_stream_t stream);
+/* Binary head on a BNRELU view: unet_head_bwd plus the BatchNorm-backward
+ * partial sums of the head input's block (dx is all of its da; bn_partials
+ * layout and finish as unet_dwconv3x3_bwd_data_bnstats).  _slabs: S, or 0. */
+int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls);
+int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls,
+                          const float* kernel, const float* prob,
+                          const float* y_true, const float* sums, float smooth,
+                          int loss_kind, float* dx, float* dkernel, float* dbias,
+                          const float* mean, const float* rstd,
+                          float* bn_partials, void* ws, size_t ws_bytes,
+                          unet_stream_t stream);
 
 /* ----- keras.metrics.MeanIoU(num_classes) — scripts/train.py:231,
  * scripts/benchmark.py:237,269.  Confusion counts (rows = true, cols =

@@ -396,28 +396,31 @@ def test_fused_sepconv_unsupported_shapes(ops):
     assert not ops.sepconv_supported(ops.View.plain(x3), 1, 16, 16, 64)  # 3 channels
 
 
+@pytest.mark.parametrize("mode", [2, 1])
 @pytest.mark.parametrize("use_bn", [True, False])
-@pytest.mark.parametrize("n,h,w,c", [(2, 8, 16, 64), (2, 5, 7, 16), (1, 4, 4, 128), (3, 8, 8, 8)])
-def test_dwconv_bwd_data_pool_bnstats(ops, use_bn, n, h, w, c):
-    """Pool-view data gradient that also emits the pooled block's BN-backward partials: dx0
-    bitwise equal to the plain launch, statistics equal to unet_bn_relu_bwd_stats's."""
-    rng = np.random.default_rng(n * 100 + h * 10 + c)
-    a, t = _view_inputs(rng, 2, n, h, w, c)
-    v = _mk_view(ops, 2, t)
+@pytest.mark.parametrize("n,h,w,c", [(2, 8, 16, 64), (2, 5, 7, 16), (1, 4, 4, 128), (3, 8, 8, 8),
+                                     (4, 64, 144, 64)])  # > 256 slabs: two-pass finish
+def test_dwconv_bwd_data_bnstats(ops, mode, use_bn, n, h, w, c):
+    """Pool / BN+ReLU-view data gradient that also emits the view block's BN-backward partials:
+    dx0 bitwise equal to the plain launch, statistics equal to unet_bn_relu_bwd_stats's."""
+    rng = np.random.default_rng(n * 100 + h * 10 + c + mode)
+    a, t = _view_inputs(rng, mode, n, h, w, c)
+    v = _mk_view(ops, mode, t)
     dk = dev(f32(rng.standard_normal((3, 3, c, 1))))
     dy = dev(f32(rng.standard_normal((n, h, w, c))))
-    init = f32(rng.standard_normal((n, 2 * h, 2 * w, c)))
+    f = 2 if mode == 2 else 1
+    init = f32(rng.standard_normal((n, f * h, f * w, c)))
     S = ops.dwconv3x3_bwd_data_bnstats_slabs(v, n, h, w)
     assert S > 0
     mean = dev(f32(rng.standard_normal(c) * 0.1))
     rstd = dev(f32(1.0 + rng.random(c)))
-    part = torch.empty(S * 2 * c, device="cuda")
+    part = torch.empty(ops.bn_stats_partials_numel(S, c), device="cuda")
     dx_f, dx_p = dev(init), dev(init)
     ops.dwconv3x3_bwd_data_bnstats(v, n, h, w, dk, dy, dx_f, mean if use_bn else None, rstd if use_bn else None,
                                    part)
     ops.dwconv3x3_bwd_data(v, n, h, w, dk, dy, dx_p)
     assert torch.equal(dx_f, dx_p)
-    m = n * 4 * h * w
+    m = n * f * f * h * w
     outs = []
     for fused in (True, False):
         dg, db, coef = (torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"),
@@ -438,3 +441,48 @@ def test_dwconv_bwd_data_pool_bnstats(ops, use_bn, n, h, w, c):
     if use_bn:
         xh = (z - host(mean)) * host(rstd)
         assert rel_err(outs[0][0], (g * xh).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("use_bn", [True, False])
+@pytest.mark.parametrize("loss_kind", [0, 1])
+def test_head_bwd_bnstats(ops, use_bn, loss_kind):
+    """Binary head backward that also emits the last block's BN-backward partials: dx / dW / db
+    bitwise equal to unet_head_bwd, statistics equal to unet_bn_relu_bwd_stats's."""
+    rng = np.random.default_rng(11 + loss_kind)
+    n, h, w, c = 2, 16, 24, 64
+    a, t = _view_inputs(rng, 1, n, h, w, c)
+    v = _mk_view(ops, 1, t)
+    k = dev(f32(rng.standard_normal((1, 1, c, 1)) * 0.2))
+    prob = dev(f32(rng.random((n, h, w, 1)) * 0.9 + 0.05))
+    yt = dev((rng.random((n, h, w, 1)) > 0.6).astype(np.float32))
+    sums = torch.empty(n * 3, device="cuda")
+    res = torch.empty(3, device="cuda")
+    ops.dice_fwd(yt, prob, n, h * w, 1, 1e-7, sums, res)
+    S = ops.head_bwd_bnstats_slabs(v, n, h, w, 1)
+    assert S > 0
+    mean = dev(f32(rng.standard_normal(c) * 0.1))
+    rstd = dev(f32(1.0 + rng.random(c)))
+    part = torch.empty(ops.bn_stats_partials_numel(S, c), device="cuda")
+    outs = []
+    for fused in (True, False):
+        dx, dk, db = torch.empty((n, h, w, c), device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
+        if fused:
+            ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db,
+                                 mean if use_bn else None, rstd if use_bn else None, part)
+        else:
+            ops.head_bwd(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db)
+        outs.append((dx, dk, db))
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)
+    m = n * h * w
+    st = []
+    for fused in (True, False):
+        dg, dbb, coef = torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"), torch.empty(3 * c, device="cuda")
+        if fused:
+            ops.bn_relu_bwd_stats_finish(part, S, m, c, mean, rstd, use_bn, dg if use_bn else None, dbb, coef)
+        else:
+            ops.bn_relu_bwd_stats(outs[1][0], t["src0"], m, c, mean, rstd, t["sc0"], t["sh0"], use_bn, 0.0, 0,
+                                  dg if use_bn else None, dbb, coef)
+        st.append((host(dg), host(dbb), host(coef)))
+    for x, y in zip(st[0], st[1]):
+        assert rel_err(x, y) < 2e-5

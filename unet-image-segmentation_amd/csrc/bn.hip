@@ -288,23 +288,21 @@ __global__ void bn_bwd_coef_kernel(const float* sums, int C, int64_t M, int use_
 
 // Statistics-only finish: the fixed-order slab reduction of (S1, S2) fused with the coefficient
 // kernel above.  Block = 16 channel quads x 32 slab groups; group g sums slabs g, g+32, ... in
-// double, then a fixed-order tree over the groups (same order as reduce_tall4).
-__global__ __launch_bounds__(512) void bn_bwd_finish_kernel(const float* __restrict__ part, int S, int C, int64_t M,
-                                                            int use_bn, const float* mean, const float* rstd,
-                                                            float* dgamma, float* dbeta, float* coef) {
-    constexpr int LQ = 16, G = 32;
-    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
-    const int c = (blockIdx.x * LQ + q) * 4;
-    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (c < C) {
-        for (int s = g; s < S; s += G) {
-            const float4 u = ld4(part + (int64_t)s * 2 * C + c);
-            const float4 v = ld4(part + (int64_t)s * 2 * C + C + c);
-            a[0] += (double)u.x; a[1] += (double)u.y; a[2] += (double)u.z; a[3] += (double)u.w;
-            a[4] += (double)v.x; a[5] += (double)v.y; a[6] += (double)v.z; a[7] += (double)v.w;
-        }
+// double, then a fixed-order tree over the groups (same order as reduce_tall4).  T = float for
+// producer slabs, double for the chunk sums of bn_bwd_chunk_kernel (large slab counts).
+template <typename T>
+__device__ __forceinline__ void load_quad(const T* p, double* a) {
+    if constexpr (sizeof(T) == 4) {
+        const float4 u = ld4(p);
+        a[0] += (double)u.x; a[1] += (double)u.y; a[2] += (double)u.z; a[3] += (double)u.w;
+    } else {
+        const double2 u = *reinterpret_cast<const double2*>(p), v = *reinterpret_cast<const double2*>(p + 2);
+        a[0] += u.x; a[1] += u.y; a[2] += v.x; a[3] += v.y;
     }
-    __shared__ double red[8][G * LQ];
+}
+template <int LQ, int G>
+__device__ __forceinline__ void tree_reduce8(double (*red)[G * LQ], double* a) {
+    const int g = threadIdx.x / LQ;
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = a[k];
     __syncthreads();
@@ -315,6 +313,50 @@ __global__ __launch_bounds__(512) void bn_bwd_finish_kernel(const float* __restr
         }
         __syncthreads();
     }
+}
+constexpr int kFinChunk = 256;  // slabs per block of the first pass
+// First pass for many slabs: block (x, y) sums slabs [256 y, 256 y + 256) of its 16 channel quads
+// (32 groups x 8 slabs, fixed order) into chunk row y (double).
+__global__ __launch_bounds__(512) void bn_bwd_chunk_kernel(const float* __restrict__ part, int S, int C,
+                                                           double* __restrict__ chunks) {
+    constexpr int LQ = 16, G = 32;
+    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
+    const int c = (blockIdx.x * LQ + q) * 4;
+    const int s0 = blockIdx.y * kFinChunk, s1 = s0 + kFinChunk < S ? s0 + kFinChunk : S;
+    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (c < C) {
+#pragma unroll 4
+        for (int s = s0 + g; s < s1; s += G) {
+            load_quad(part + (int64_t)s * 2 * C + c, a);
+            load_quad(part + (int64_t)s * 2 * C + C + c, a + 4);
+        }
+    }
+    __shared__ double red[8][G * LQ];
+    tree_reduce8<LQ, G>(red, a);
+    if (g != 0 || c >= C) return;
+    double* out = chunks + (int64_t)blockIdx.y * 2 * C;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        out[c + k] = red[k][q];
+        out[C + c + k] = red[4 + k][q];
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(512) void bn_bwd_finish_kernel(const T* __restrict__ part, int S, int C, int64_t M,
+                                                            int use_bn, const float* mean, const float* rstd,
+                                                            float* dgamma, float* dbeta, float* coef) {
+    constexpr int LQ = 16, G = 32;
+    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
+    const int c = (blockIdx.x * LQ + q) * 4;
+    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (c < C) {
+        for (int s = g; s < S; s += G) {
+            load_quad(part + (int64_t)s * 2 * C + c, a);
+            load_quad(part + (int64_t)s * 2 * C + C + c, a + 4);
+        }
+    }
+    __shared__ double red[8][G * LQ];
+    tree_reduce8<LQ, G>(red, a);
     if (g != 0 || c >= C) return;
     const float invM = 1.0f / (float)M;
 #pragma unroll
@@ -469,7 +511,7 @@ int bn_relu_bwd_impl(const float* da, const float* z, int64_t m, int c, const fl
 #undef UNET_BNB
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(reduce)");
     if (coef_out && vec) {  // statistics-only entry (unet_bn_relu_bwd_stats): reduce + coefficients
-        bn_bwd_finish_kernel<<<(unsigned)cdiv(c / 4, 16), 512, 0, st>>>(part, (int)p.chunks, c, m, use_bn, mean, rstd,
+        bn_bwd_finish_kernel<float><<<(unsigned)cdiv(c / 4, 16), 512, 0, st>>>(part, (int)p.chunks, c, m, use_bn, mean, rstd,
                                                                         dgamma, dbeta, coef_out);
         UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats(finish)");
         return 0;
@@ -511,14 +553,31 @@ extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int 
                             nullptr, ws, ws_bytes, stream);
 }
 
-extern "C" int unet_bn_relu_bwd_stats_finish(const float* partials, int S, int64_t m, int c, const float* mean,
+extern "C" size_t unet_bn_stats_partials_size(int S, int c) {
+    if (S <= 0 || c <= 0) return 0;
+    size_t b = align_up((size_t)S * 2 * c * sizeof(float), 256);
+    if (S > kFinChunk) b += (size_t)cdiv(S, kFinChunk) * 2 * c * sizeof(double);
+    return b;
+}
+
+extern "C" int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, int c, const float* mean,
                                              const float* rstd, int use_bn, float* dgamma, float* dbeta, float* coef,
                                              unet_stream_t stream) {
     UNET_CHECK_ARG(partials && coef && S > 0 && m > 0 && c > 0, "unet_bn_relu_bwd_stats_finish: bad args");
     UNET_CHECK_ARG(c % 4 == 0, "unet_bn_relu_bwd_stats_finish: channels must be a multiple of 4");
     UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_relu_bwd_stats_finish: use_bn needs mean/rstd");
-    bn_bwd_finish_kernel<<<(unsigned)cdiv(c / 4, 16), 512, 0, as_stream(stream)>>>(partials, S, c, m, use_bn, mean,
-                                                                                   rstd, dgamma, dbeta, coef);
+    hipStream_t st = as_stream(stream);
+    const unsigned gx = (unsigned)cdiv(c / 4, 16);
+    if (S <= kFinChunk) {
+        bn_bwd_finish_kernel<float><<<gx, 512, 0, st>>>(partials, S, c, m, use_bn, mean, rstd, dgamma, dbeta, coef);
+    } else {  // two passes: 256-slab chunk sums (double, in the buffer's tail), then the finish
+        const int nch = (int)cdiv(S, kFinChunk);
+        double* chunks = reinterpret_cast<double*>(reinterpret_cast<char*>(partials) +
+                                                   align_up((size_t)S * 2 * c * sizeof(float), 256));
+        bn_bwd_chunk_kernel<<<dim3(gx, (unsigned)nch), 512, 0, st>>>(partials, S, c, chunks);
+        UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats_finish(chunks)");
+        bn_bwd_finish_kernel<double><<<gx, 512, 0, st>>>(chunks, nch, c, m, use_bn, mean, rstd, dgamma, dbeta, coef);
+    }
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats_finish");
     return 0;
 }

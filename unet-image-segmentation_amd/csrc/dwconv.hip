@@ -381,8 +381,9 @@ size_t dw_tiled_filter_partials(int N, int H, int W, int C);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
 bool dw_tiled_ok(int C);
-int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
-                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st);
+int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
+                              const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
+                              hipStream_t st);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
 
 static int check_dims(const unet_view* x, int n, int h, int w, const char* op) {
@@ -445,7 +446,8 @@ extern "C" int unet_dwconv3x3_bwd_data(const unet_view* x, int n, int h, int w, 
 }
 
 extern "C" int unet_dwconv3x3_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w) {
-    if (!x || x->mode != UNET_VIEW_POOL_BNRELU || n <= 0 || h <= 0 || w <= 0) return 0;
+    if (!x || (x->mode != UNET_VIEW_POOL_BNRELU && x->mode != UNET_VIEW_BNRELU) || n <= 0 || h <= 0 || w <= 0)
+        return 0;
     if (!view_vec(x) || !dw_tiled_ok(x->c0)) return 0;
     return (int)dw_tiled_ntiles(n, h, w, x->c0);
 }
@@ -457,10 +459,10 @@ extern "C" int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h,
     if (check_view(x, op) || check_dims(x, n, h, w, op)) return -1;
     UNET_CHECK_ARG(dw_kernel && dy && dx0 && bn_partials, "%s: null pointer", op);
     UNET_CHECK_ARG(unet_dwconv3x3_bwd_data_bnstats_slabs(x, n, h, w) > 0,
-                   "%s: needs a POOL_BNRELU view with channels %% 4 == 0 (tiled path)", op);
+                   "%s: needs a POOL_BNRELU or BNRELU view with channels %% 4 == 0 (tiled path)", op);
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "%s: mean and rstd go together", op);
     const DView v = make_dview(*x);
-    return dw_tiled_bwd_data_bnstats(v, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
+    return dw_tiled_bwd_data_bnstats(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
                                      as_stream(stream));
 }
 

@@ -18,8 +18,9 @@ int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const
 int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
                       float* dx0, float* dx1, hipStream_t st);
 size_t dw_tiled_filter_partials(int N, int H, int W, int C);
-int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
-                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st);
+int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
+                              const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
+                              hipStream_t st);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
@@ -164,9 +165,10 @@ __global__ __launch_bounds__(256, 3) void dw_tile_fwd(DView v, int N, int H, int
     }
 }
 
-// STATS (POOL view only): this kernel is the last writer of the pooled block's da (it adds the
-// pooled half to the stored skip half) and reads that block's raw z for the argmax, so it also
-// emits the block's BatchNorm-backward partial sums over its tile: bnpart[tile][0][c] = sum g,
+// STATS (POOL or BNRELU view): this kernel is the last writer of the view's block's da (POOL: it
+// adds the pooled half to the stored skip half and reads the block's raw z for the argmax anyway;
+// BNRELU: it writes the whole da and reads z for the mask), so it also emits that block's
+// BatchNorm-backward partial sums over its tile: bnpart[tile][0][c] = sum g,
 // bnpart[tile][1][c] = sum g * xhat with g = da * [z*sc+sh > 0], xhat = (z - mu) * rs (the
 // unet_bn_relu_bwd_stats reduction, without its separate pass over (da, z)).
 template <int MODE, bool DROP, int QT, bool STATS = false>
@@ -230,6 +232,18 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
         }
         if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
             st4(dx0 + (int64_t)p * C + c, acc);
+            if constexpr (STATS && MODE == UNET_VIEW_BNRELU) {  // dx0 is the whole da of the view's block
+                const float4 zr = ld4(v.src0 + (int64_t)p * C + c);
+                const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
+                const float4 gm = make_float4(fmaf(zr.x, sc.x, sh.x) > 0.f ? acc.x : 0.f,
+                                              fmaf(zr.y, sc.y, sh.y) > 0.f ? acc.y : 0.f,
+                                              fmaf(zr.z, sc.z, sh.z) > 0.f ? acc.z : 0.f,
+                                              fmaf(zr.w, sc.w, sh.w) > 0.f ? acc.w : 0.f);
+                s1 = add4(s1, gm);
+                const float4 xh = make_float4((zr.x - smu.x) * srs.x, (zr.y - smu.y) * srs.y,
+                                              (zr.z - smu.z) * srs.z, (zr.w - smu.w) * srs.w);
+                s2 = fma4(gm, xh, s2);
+            }
         } else if constexpr (MODE == UNET_VIEW_CONCAT) {
             if (c < v.c0)
                 st4(dx0 + (int64_t)p * v.c0 + c, acc);
@@ -440,13 +454,18 @@ int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, 
     return 0;
 }
 
-int dw_tiled_bwd_data_bnstats(const DView& v, bool drop, int N, int H, int W, const float* K, const float* dY,
-                              float* dx0, const float* mu, const float* rs, float* bnpart, hipStream_t st) {
+int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
+                              const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
+                              hipStream_t st) {
     TilePlan p = tile_plan(N, H, W, v.C);
     dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
-#define UNET_BNS(D, Q)                                                                                       \
-    dw_tile_bwd_data<UNET_VIEW_POOL_BNRELU, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, K, \
-                                                                              dY, dx0, nullptr, mu, rs, bnpart)
+#define UNET_BNS(D, Q)                                                                                            \
+    if (mode == UNET_VIEW_POOL_BNRELU)                                                                            \
+        dw_tile_bwd_data<UNET_VIEW_POOL_BNRELU, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, \
+                                                                                  K, dY, dx0, nullptr, mu, rs, bnpart); \
+    else                                                                                                          \
+        dw_tile_bwd_data<UNET_VIEW_BNRELU, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, K,   \
+                                                                             dY, dx0, nullptr, mu, rs, bnpart)
 #define UNET_BNS_QT(D)                      \
     switch (p.qt) {                          \
         case 16: UNET_BNS(D, 16); break;     \

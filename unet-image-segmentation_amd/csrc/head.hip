@@ -187,12 +187,17 @@ __device__ __forceinline__ float loss_grad(float t, const float* s3, float smoot
 //   phase 2: one lane per (pixel, channel quad), coalesced: dx = W dlogit, and
 //            dW += relu(bn(z)) * dlogit accumulated in registers across tiles;
 //   end: fixed-order LDS reduction -> per-block partials of dW (Cin) and db (1).
-template <int MODE, int LOSS>
+// STATS (BNRELU view): dx is the whole da of the last decoder block, so the kernel also emits
+// that block's BatchNorm-backward partial sums (bnpart[block][0][c] = sum g, [1][c] = sum g*xhat,
+// g = dx*[z*sc+sh > 0], xhat = (z-mu)*rs) instead of leaving them to a pass over (dx, z).
+template <int MODE, int LOSS, bool STATS = false>
 __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int64_t hw, const float* __restrict__ W,
                                                         const float* __restrict__ prob, const float* __restrict__ yt,
                                                         const float* __restrict__ sums, float smooth, float gscale,
                                                         float* __restrict__ dx, float* __restrict__ part_w,
-                                                        float* __restrict__ part_b) {
+                                                        float* __restrict__ part_b, const float* __restrict__ mu = nullptr,
+                                                        const float* __restrict__ rs = nullptr,
+                                                        float* __restrict__ bnpart = nullptr) {
     __shared__ float dls[256];
     __shared__ float4 red[256];
     const int Cin = v.c0, CQ = Cin / 4;
@@ -200,6 +205,15 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int6
     const float4 w4 = ld4(W + 4 * kq);
     float4 dw = f4(0.f);
     float db = 0.f;
+    float4 s1 = f4(0.f), s2 = f4(0.f), hsc = f4(1.f), hsh = f4(0.f), smu = f4(0.f), srs = f4(0.f);
+    if constexpr (STATS) {
+        hsc = ld4(v.sc0 + 4 * kq);
+        hsh = ld4(v.sh0 + 4 * kq);
+        if (mu) {
+            smu = ld4(mu + 4 * kq);
+            srs = ld4(rs + 4 * kq);
+        }
+    }
     for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
         __syncthreads();
         {
@@ -218,9 +232,41 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int6
             const int64_t m = m0 + p;
             if (m >= M) break;
             const float dl = dls[p];
-            const float4 a = row_load4<MODE, false>(v, m, 4 * kq);
-            dw = fma4(a, f4(dl), dw);
-            st4(dx + m * Cin + 4 * kq, mul4(w4, f4(dl)));
+            if constexpr (STATS) {
+                const float4 zr = ld4(v.src0 + m * Cin + 4 * kq);
+                const float4 a = bnrelu4(zr, hsc, hsh);
+                dw = fma4(a, f4(dl), dw);
+                const float4 d = mul4(w4, f4(dl));
+                st4(dx + m * Cin + 4 * kq, d);
+                const float4 gm = make_float4(a.x > 0.f ? d.x : 0.f, a.y > 0.f ? d.y : 0.f, a.z > 0.f ? d.z : 0.f,
+                                              a.w > 0.f ? d.w : 0.f);
+                s1 = add4(s1, gm);
+                const float4 xh = make_float4((zr.x - smu.x) * srs.x, (zr.y - smu.y) * srs.y, (zr.z - smu.z) * srs.z,
+                                              (zr.w - smu.w) * srs.w);
+                s2 = fma4(gm, xh, s2);
+            } else {
+                const float4 a = row_load4<MODE, false>(v, m, 4 * kq);
+                dw = fma4(a, f4(dl), dw);
+                st4(dx + m * Cin + 4 * kq, mul4(w4, f4(dl)));
+            }
+        }
+    }
+    if constexpr (STATS) {  // fixed-order per-channel-quad sums of the block's threads
+        __syncthreads();
+        red[threadIdx.x] = s1;
+        __syncthreads();
+        if (threadIdx.x < CQ) {
+            float4 t = red[threadIdx.x];
+            for (int q = threadIdx.x + CQ; q < 256; q += CQ) t = add4(t, red[q]);
+            st4(bnpart + (int64_t)blockIdx.x * 2 * Cin + 4 * threadIdx.x, t);
+        }
+        __syncthreads();
+        red[threadIdx.x] = s2;
+        __syncthreads();
+        if (threadIdx.x < CQ) {
+            float4 t = red[threadIdx.x];
+            for (int q = threadIdx.x + CQ; q < 256; q += CQ) t = add4(t, red[q]);
+            st4(bnpart + (int64_t)blockIdx.x * 2 * Cin + Cin + 4 * threadIdx.x, t);
         }
     }
     __syncthreads();
@@ -442,10 +488,49 @@ extern "C" size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls
     return align_up(fused > gen ? fused : gen, 256);
 }
 
+namespace {
+int head_bwd_grid(int64_t M) {
+    const int64_t g = cdiv(M, 256);
+    return (int)(g > 1024 ? 1024 : g);
+}
+int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
+                  const float* y_true, const float* sums, float smooth, int loss_kind, float* dx, float* dkernel,
+                  float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs, float* bnpart,
+                  unet_stream_t stream);
+}  // namespace
+
+extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls) {
+    if (!x || x->mode != UNET_VIEW_BNRELU || ncls != 1 || n <= 0 || h <= 0 || w <= 0) return 0;
+    if (x->c0 % 4 || x->c0 > kMaxCin || 256 % (x->c0 / 4)) return 0;
+    return head_bwd_grid((int64_t)n * h * w);
+}
+
+extern "C" int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
+                                     const float* prob, const float* y_true, const float* sums, float smooth,
+                                     int loss_kind, float* dx, float* dkernel, float* dbias, const float* mean,
+                                     const float* rstd, float* bn_partials, void* ws, size_t ws_bytes,
+                                     unet_stream_t stream) {
+    UNET_CHECK_ARG(unet_head_bwd_bnstats_slabs(x, n, h, w, ncls) > 0,
+                   "unet_head_bwd_bnstats: needs a binary head on a BNRELU view with Cin %% 4 == 0");
+    UNET_CHECK_ARG(bn_partials, "unet_head_bwd_bnstats: null bn_partials");
+    UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_head_bwd_bnstats: mean and rstd go together");
+    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, dx, dkernel, dbias, ws,
+                         ws_bytes, mean, rstd, bn_partials, stream);
+}
+
 extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
                              const float* prob, const float* y_true, const float* sums, float smooth, int loss_kind,
                              float* dx, float* dkernel, float* dbias, void* ws, size_t ws_bytes,
                              unet_stream_t stream) {
+    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, dx, dkernel, dbias, ws,
+                         ws_bytes, nullptr, nullptr, nullptr, stream);
+}
+
+namespace {
+int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
+                  const float* y_true, const float* sums, float smooth, int loss_kind, float* dx, float* dkernel,
+                  float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs, float* bnpart,
+                  unet_stream_t stream) {
     if (check_view(x, "unet_head_bwd", true)) return -1;
     UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
                    "unet_head_bwd: input view must be PLAIN or BNRELU");
@@ -462,14 +547,19 @@ extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, 
     const DView v = make_dview(*x);
     const int CQ = x->c0 / 4;
     if (ncls == 1 && 256 % CQ == 0) {
-        int64_t g = cdiv(M, 256);
-        const int grid = (int)(g > 1024 ? 1024 : g);
+        const int grid = head_bwd_grid(M);
         float* part_w = static_cast<float*>(ws);
         float* part_b = part_w + align_up((size_t)grid * x->c0, 64);
 #define UNET_HB1(MODE, L)                                                                                     \
     head_bwd1_kernel<MODE, L><<<grid, 256, 0, st>>>(v, M, hw, kernel, prob, y_true, sums, smooth, gscale, dx, \
                                                      part_w, part_b)
-        if (x->mode == UNET_VIEW_BNRELU) {
+#define UNET_HB1S(L)                                                                                          \
+    head_bwd1_kernel<UNET_VIEW_BNRELU, L, true><<<grid, 256, 0, st>>>(v, M, hw, kernel, prob, y_true, sums,   \
+                                                                      smooth, gscale, dx, part_w, part_b, mu, rs, bnpart)
+        if (bnpart) {
+            if (loss_kind == UNET_LOSS_DICE) UNET_HB1S(UNET_LOSS_DICE);
+            else UNET_HB1S(UNET_LOSS_IOU);
+        } else if (x->mode == UNET_VIEW_BNRELU) {
             if (loss_kind == UNET_LOSS_DICE) UNET_HB1(UNET_VIEW_BNRELU, UNET_LOSS_DICE);
             else UNET_HB1(UNET_VIEW_BNRELU, UNET_LOSS_IOU);
         } else {
@@ -477,6 +567,7 @@ extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, 
             else UNET_HB1(UNET_VIEW_PLAIN, UNET_LOSS_IOU);
         }
 #undef UNET_HB1
+#undef UNET_HB1S
         UNET_CHECK_LAUNCH("unet_head_bwd");
         int rc = reduce_slabs(part_w, grid, x->c0, dkernel, x->c0, x->c0, st);
         if (rc) return rc;
@@ -504,6 +595,7 @@ extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, 
     if (rc) return rc;
     return colsum(dlogit, M, ncls, dbias, ws2, ws2_bytes, st);
 }
+}  // namespace
 
 extern "C" int unet_meaniou_update(const float* y_true, const float* y_pred, int64_t count, int num_classes,
                                    float threshold, uint64_t* confusion, unet_stream_t stream) {

@@ -47,28 +47,33 @@ __global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restri
     store_out(out, l + 3, row, ld_out, a3);
 }
 
-// Tall reductions (few outputs, many slabs): block = 16 output quads x 32 slab groups; group g
-// sums s = g, g+32, ... and a fixed-order tree adds the 32 group partials.
-__global__ __launch_bounds__(512) void reduce_tall4_kernel(const float* __restrict__ part, int S, int64_t L,
-                                                           float* __restrict__ out, int64_t row, int64_t ld_out) {
-    constexpr int LQ = 16, G = 32;
+// Grouped reductions: block = (512/G) output quads x G slab groups; group g sums slabs g, g+G, ...
+// in increasing order (4 loads in flight), then a fixed-order tree adds the G group partials.  G
+// is picked so that enough loads are in flight chip-wide (few outputs -> more groups).
+template <int G>
+__global__ __launch_bounds__(512) void reduce_grp4_kernel(const float* __restrict__ part, int S, int64_t L,
+                                                          float* __restrict__ out, int64_t row, int64_t ld_out) {
+    constexpr int LQ = 512 / G;
     const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
     const int64_t l = ((int64_t)blockIdx.x * LQ + q) * 4;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (l < L) {
         int s = g;
-        for (; s + G < S; s += 2 * G) {
-            const float4 v0 = ld4(part + (int64_t)s * L + l);
-            const float4 v1 = ld4(part + (int64_t)(s + G) * L + l);
-            a[0] += (double)v0.x; a[1] += (double)v0.y; a[2] += (double)v0.z; a[3] += (double)v0.w;
-            a[0] += (double)v1.x; a[1] += (double)v1.y; a[2] += (double)v1.z; a[3] += (double)v1.w;
+        for (; s + 3 * G < S; s += 4 * G) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = ld4(part + (int64_t)(s + u * G) * L + l);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a[0] += (double)v[u].x; a[1] += (double)v[u].y; a[2] += (double)v[u].z; a[3] += (double)v[u].w;
+            }
         }
-        if (s < S) {
+        for (; s < S; s += G) {
             const float4 v0 = ld4(part + (int64_t)s * L + l);
             a[0] += (double)v0.x; a[1] += (double)v0.y; a[2] += (double)v0.z; a[3] += (double)v0.w;
         }
     }
-    __shared__ double red[4][G * LQ];
+    __shared__ double red[4][512];
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
     __syncthreads();
@@ -84,7 +89,6 @@ __global__ __launch_bounds__(512) void reduce_tall4_kernel(const float* __restri
         for (int k = 0; k < 4; ++k) store_out(out, l + k, row, ld_out, red[k][q]);
     }
 }
-
 // Scalar fallback for L % 4 != 0: block = 64 outputs x 16 slab groups.
 __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L,
                                                             float* __restrict__ out, int64_t row, int64_t ld_out) {
@@ -134,10 +138,21 @@ int check_view(const unet_view* v, const char* op, bool need_vec4) {
 int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream) {
     UNET_CHECK_ARG(S >= 1 && L >= 1 && row >= 1, "reduce_slabs: bad sizes");
     const bool vec = L % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
-    if (vec && (cdiv(L, 1024) >= 64 || S <= 32)) {
-        reduce_cols4_kernel<<<(unsigned)cdiv(L, 1024), 256, 0, stream>>>(part, S, L, out, row, ld_out);
-    } else if (vec) {
-        reduce_tall4_kernel<<<(unsigned)cdiv(L, 64), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+    if (vec) {
+        // groups per output quad: enough threads for ~256K loads in flight, at most 32, at most S
+        const int64_t quads = L / 4;
+        int G = 1;
+        while (G < 32 && G < S && quads * G < 262144) G *= 2;
+        if (G == 1 || S <= 8)
+            reduce_cols4_kernel<<<(unsigned)cdiv(L, 1024), 256, 0, stream>>>(part, S, L, out, row, ld_out);
+        else if (G == 2 || G == 4)
+            reduce_grp4_kernel<4><<<(unsigned)cdiv(quads, 128), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+        else if (G == 8)
+            reduce_grp4_kernel<8><<<(unsigned)cdiv(quads, 64), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+        else if (G == 16)
+            reduce_grp4_kernel<16><<<(unsigned)cdiv(quads, 32), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+        else
+            reduce_grp4_kernel<32><<<(unsigned)cdiv(quads, 16), 512, 0, stream>>>(part, S, L, out, row, ld_out);
     } else {
         reduce_slabs_kernel<<<(unsigned)cdiv(L, 64), 1024, 0, stream>>>(part, S, L, out, row, ld_out);
     }

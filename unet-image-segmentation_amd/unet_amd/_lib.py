@@ -63,6 +63,7 @@ SIGNATURES = {
     "unet_bn_relu_bwd_workspace": (c_size_t, [c_int64, c_int]),
     "unet_bn_relu_bwd": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                  c_size_t, P]),
+    "unet_bn_stats_partials_size": (c_size_t, [c_int, c_int]),
     "unet_bn_relu_bwd_stats_finish": (c_int, [P, c_int, c_int64, c_int, P, P, c_int, P, P, P, P]),
     "unet_bn_relu_bwd_stats": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                        c_size_t, P]),
@@ -75,6 +76,9 @@ SIGNATURES = {
     "unet_dice_workspace": (c_size_t, [c_int, c_int64, c_int]),
     "unet_dice_fwd": (c_int, [P, P, c_int, c_int64, c_int, c_float, P, P, P, c_size_t, P]),
     "unet_head_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "unet_head_bwd_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int, c_int]),
+    "unet_head_bwd_bnstats": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, P, P, P, P, P, P,
+                                      P, c_size_t, P]),
     "unet_head_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, P, P, P, P, c_size_t,
                               P]),
     "unet_meaniou_update": (c_int, [P, P, c_int64, c_int, c_float, P, P]),

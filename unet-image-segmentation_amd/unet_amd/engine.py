@@ -144,8 +144,8 @@ class UNetEngine:
         self.fuse_sepconv = "auto"
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
-        # BN-backward statistics of a pooled encoder block emitted by the launch that completes its
-        # da (the next block's depthwise data gradient through the max-pool), not by a pass over (da, z)
+        # BN-backward statistics of a block emitted by the launch that completes its da (the next
+        # block's depthwise data gradient through BN+ReLU or the max-pool), not by a pass over (da, z)
         self.fuse_bn_stats = os.environ.get("UNET_FUSE_BN_STATS", "1") != "0"
 
     # ------------------------------------------------------------------ weights ------
@@ -267,15 +267,17 @@ class UNetEngine:
             ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
         return View.bnrelu(bb.z, bb.scale, bb.shift)
 
-    def _wts(self, b: Block):
-        """(depthwise, pointwise) kernels of a block as the kernels see them."""
+    def _wts(self, b: Block, refresh: bool = True):
+        """(depthwise, pointwise) kernels of a block as the kernels see them.  refresh=False (the
+        backward of the forward that filled them) skips re-mirroring the padded image-block copy."""
         dk = self.vars[f"{b.name}_sepconv/depthwise_kernel"]
         pk = self.vars[f"{b.name}_sepconv/pointwise_kernel"]
         if not b.wcin:
             return dk, pk
         pad = self._pad_w
-        pad["dk"][:, :, :b.wcin].copy_(dk)
-        pad["pk"][:, :, :b.wcin].copy_(pk)
+        if refresh:
+            pad["dk"][:, :, :b.wcin].copy_(dk)
+            pad["pk"][:, :, :b.wcin].copy_(pk)
         return pad["dk"], pad["pk"]
 
     def _gwts(self, b: Block):
@@ -367,9 +369,10 @@ class UNetEngine:
                 self.grad_hook(self.train_layout.offsets[name])
 
     def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0,
-                   pool_target: Optional[BlockBufs] = None):
-        """Backward of one conv_block.  pool_target: the encoder block whose output view_in max-pools;
-        dx0 (its da) is completed here and, on the fused path, so are its BN-backward partials."""
+                   stats_target: Optional[BlockBufs] = None):
+        """Backward of one conv_block.  stats_target: the block whose output view_in reads (through
+        BN+ReLU or the max-pool) when this launch completes its da (dx0); on the fused path the
+        depthwise data gradient then also emits that block's BN-backward partials."""
         n = A.n
         h, w = self._dims(b.level)
         m = n * h * w
@@ -383,7 +386,7 @@ class UNetEngine:
             dgamma, dbeta = self.gvars[f"{b.name}_bn/gamma"], self.gvars[f"{b.name}_bn/beta"]
         else:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
-        dk, pk = self._wts(b)
+        dk, pk = self._wts(b, refresh=False)
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
             if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
@@ -416,11 +419,11 @@ class UNetEngine:
             weight_grads()
         if dx0 is not None:
             S = 0
-            if pool_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
+            if stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
                 S = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w)
             if S > 0:
-                tb = pool_target
-                need = S * 2 * view_in.channels
+                tb = stats_target
+                need = ops.bn_stats_partials_numel(S, view_in.channels)
                 if tb.bnpart is None or tb.bnpart.numel() < need:
                     tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
                 ops.dwconv3x3_bwd_data_bnstats(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
@@ -441,14 +444,27 @@ class UNetEngine:
         seeds = self._last_seeds
         drop = seeds is not None and self.dropout_rate > 0.0
         last = self.dec[-1][4]
-        ops.head_bwd(self._view_of(A, last), n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
-                     A.prob, y_true, A.sums, SMOOTH, loss_kind, A.blocks[last.name].da,
-                     self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"])
+        hv, lb = self._view_of(A, last), A.blocks[last.name]
+        S = (ops.head_bwd_bnstats_slabs(hv, n, self.h, self.w, self.num_classes)
+             if self.fuse_bn_stats and self.fuse_bn_bwd else 0)
+        if S > 0:  # the head's dx is all of the last block's da: emit its BN-backward partials too
+            need = ops.bn_stats_partials_numel(S, hv.channels)
+            if lb.bnpart is None or lb.bnpart.numel() < need:
+                lb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+            ops.head_bwd_bnstats(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"], A.prob,
+                                 y_true, A.sums, SMOOTH, loss_kind, lb.da, self.gvars["output_mask/kernel"],
+                                 self.gvars["output_mask/bias"], lb.mean if self.use_bn else None,
+                                 lb.rstd if self.use_bn else None, lb.bnpart)
+            lb.bn_slabs = S
+        else:
+            ops.head_bwd(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
+                         A.prob, y_true, A.sums, SMOOTH, loss_kind, lb.da,
+                         self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"])
         self._grads_ready("output_mask/kernel")
         nd = len(self.dec)
         for i in reversed(range(nd)):
             stage, fi, cin, b1, b2 = self.dec[i]
-            self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da)
+            self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da, stats_target=A.blocks[b1.name])
             enc_b2 = self.enc[len(self.enc) - 1 - i][2]
             sk = A.blocks[enc_b2.name]
             vin = View.concat(A.up[stage], sk.z, sk.scale, sk.shift)
@@ -468,16 +484,16 @@ class UNetEngine:
         b1, b2 = self.bneck
         self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da,
                         drop_rate=self.dropout_rate if drop else 0.0,
-                        drop_seed=seeds["bneck_dropout"] if drop else 0)
+                        drop_seed=seeds["bneck_dropout"] if drop else 0, stats_target=A.blocks[b1.name])
         e4 = A.blocks[self.enc[-1][2].name]
         # pooled half ACCUMULATES into the encoder block's da (the skip half is already there)
-        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, pool_target=e4)
+        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, stats_target=e4)
         for j in reversed(range(len(self.enc))):
             stage, e1, e2 = self.enc[j]
-            self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da)
+            self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da, stats_target=A.blocks[e1.name])
             if j > 0:
                 pb = A.blocks[self.enc[j - 1][2].name]
-                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, pool_target=pb)
+                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
         if self.overlap:

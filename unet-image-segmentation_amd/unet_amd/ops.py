@@ -218,7 +218,7 @@ def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Te
     _check(dk, "depthwise_kernel", 9 * C)
     _check(dy, "dy", n * h * w * C)
     _check(dx0, "dx0")
-    _check(partials, "bn_partials", S * 2 * C)
+    _check(partials, "bn_partials", bn_stats_partials_numel(S, C))
     vs = x.c_struct()
     m = n * h * w
     nb = 8.0 * m * C + 3.0 * x.src_bytes(n, h, w) + 4.0 * S * 2 * C
@@ -326,10 +326,15 @@ def bn_relu_bwd_stats(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, 
           _ptr(dgamma), _ptr(dbeta), _ptr(coef), ws, wsb, _stream())
 
 
+def bn_stats_partials_numel(S: int, c: int) -> int:
+    """Floats of a producer-side BN partials buffer of S slabs (slabs + finish scratch)."""
+    return L.query("unet_bn_stats_partials_size", S, c) // 4
+
+
 def bn_relu_bwd_stats_finish(partials: Tensor, S: int, m: int, c: int, mean, rstd, use_bn: bool, dgamma, dbeta,
                              coef: Tensor):
     """bn_relu_bwd_stats's outputs from producer-side partial slabs ([S][2][c])."""
-    _check(partials, "bn_partials", S * 2 * c)
+    _check(partials, "bn_partials", bn_stats_partials_numel(S, c))
     _check(coef, "coef", 3 * c)
     _call("unet_bn_relu_bwd_stats_finish", (2.0 * S * c, 8.0 * S * c), _ptr(partials), S, m, c, _ptr(mean),
           _ptr(rstd), int(bool(use_bn)), _ptr(dgamma), _ptr(dbeta), _ptr(coef), _stream())
@@ -410,6 +415,27 @@ def head_bwd(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, su
     _call("unet_head_bwd", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
           ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums),
            float(smooth), int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), ws, wsb, _stream())
+
+
+def head_bwd_bnstats_slabs(x: View, n, h, w, ncls) -> int:
+    vs = x.c_struct()
+    return L.query("unet_head_bwd_bnstats_slabs", ctypes.byref(vs), n, h, w, ncls)
+
+
+def head_bwd_bnstats(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, sums: Tensor, smooth: float,
+                     loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor, mean, rstd, partials: Tensor):
+    """head_bwd that also emits the BN-backward partials of the head input's block."""
+    S = head_bwd_bnstats_slabs(x, n, h, w, ncls)
+    _check(prob, "prob", n * h * w * ncls)
+    _check(y_true, "y_true", n * h * w * ncls)
+    _check(dx, "dx", n * h * w * x.c0)
+    _check(partials, "bn_partials", bn_stats_partials_numel(S, x.c0))
+    ws, wsb = _ws(L.query("unet_head_bwd_workspace", n, h, w, x.c0, ncls), prob.device)
+    vs = x.c_struct()
+    m = n * h * w
+    _call("unet_head_bwd_bnstats", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
+          ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums), float(smooth),
+          int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), _ptr(mean), _ptr(rstd), _ptr(partials), ws, wsb, _stream())
 
 
 def meaniou_update(y_true: Tensor, y_pred: Tensor, num_classes: int, threshold: Optional[float],
