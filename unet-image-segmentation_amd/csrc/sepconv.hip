@@ -41,7 +41,7 @@ struct SepArgs {
 // LDS allows the matching blocks per CU
 constexpr int sep_min_waves(int BN, int WN) { return WN == 2 ? (BN == 64 ? 3 : 2) : (BN == 128 ? 4 : 2); }
 
-template <int MODE, bool DROP, int EPI, int BN, int WN, bool WRITE_Y, int SCHED = 0>
+template <int MODE, bool DROP, int EPI, int BN, int WN, bool WRITE_Y>
 __global__ __launch_bounds__(128 * WN, sep_min_waves(BN, WN)) void sepconv_fwd_kernel(SepArgs g) {
     constexpr int NT = 128 * WN;              // threads
     constexpr int LB = BN + 4;
@@ -280,28 +280,11 @@ __global__ __launch_bounds__(128 * WN, sep_min_waves(BN, WN)) void sepconv_fwd_k
         load_b((kt + 1) * BK);
         mfma_kg(buf, 0);
         dw_stage(buf ^ 1);
-        if constexpr (SCHED == 1) {
-            // interleave the stage's MFMAs with the depthwise VALU / LDS work of the next stage
-#pragma unroll
-            for (int i = 0; i < 4 * TN; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-            }
-        }
         __syncthreads();  // every wave is done reading the halo of stage kt+1
         mfma_kg(buf, 1);
         store_halo(hr, buf);
         store_b(buf ^ 1);
         if (kt + 1 < nk) store_y((kt + 1) * BK);
-        if constexpr (SCHED == 1) {
-#pragma unroll
-            for (int i = 0; i < 4 * TN; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            }
-        }
         __syncthreads();
     }
 
