@@ -131,6 +131,15 @@ size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout);
 int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
                               int cin, int cout, float* d_pw_kernel,
                               void* ws, size_t ws_bytes, unet_stream_t stream);
+/* Same gradient with dz formed on load from (da, z) and the coefficients of
+ * unet_bn_relu_bwd_stats (no dropout on the block output), so the data-gradient
+ * GEMM need not store dz (dz = NULL there).  Workspace as unet_pointwise_bwd_filter. */
+int unet_pointwise_bwd_filter_bnrelu(const float* y, const float* da,
+                                     const float* z, int64_t m, int cin, int cout,
+                                     const float* scale, const float* shift,
+                                     const float* coef, float* d_pw_kernel,
+                                     void* ws, size_t ws_bytes,
+                                     unet_stream_t stream);
 
 /* Fused SeparableConv2D: depthwise 3x3 of the view -> pointwise 1x1 (+ BatchNorm partials as
  * unet_pointwise_fwd), the depthwise result never leaving the chip except as the optional `y`

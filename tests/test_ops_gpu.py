@@ -241,6 +241,13 @@ def test_pointwise_bwd_data_bnrelu(ops, use_bn, drop, m, cin, cout):
     assert rel_err(host(dz), rz.reshape(m, c)) < 1e-4
     ry = rz.reshape(m, c) @ pk[0, 0].T
     assert rel_err(host(dy), ry) < 1e-4
+    if drop == 0.0 and cin % 4 == 0 and c % 4 == 0:
+        # the weight gradient forming dz itself from (da, z) equals the one reading the stored dz
+        y = dev(f32(rng.standard_normal((m, cin))))
+        g1, g2 = torch.empty((cin, c), device="cuda"), torch.empty((cin, c), device="cuda")
+        ops.pointwise_bwd_filter(y, dz, m, cin, c, g1)
+        ops.pointwise_bwd_filter_bnrelu(y, dev(da), dev(z), m, cin, c, ts, th, coef, g2)
+        assert torch.equal(g1, g2)
 
 
 @pytest.mark.parametrize("mode,drop", [(1, 0.0), (1, 0.2), (0, 0.0)])

@@ -272,7 +272,10 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(RowsArgs g) {
 }
 
 // --------------------------------------------------------------------------------- wgrad ----
-enum { W_PLAIN = 0, W_BNRELU = 1, W_UNSHUFFLE = 2 };
+// W_BNBWD (B operand, vectorised kernel only): B = dz of a BatchNorm + ReLU output formed on load
+// from da (b.src0) and the raw z exactly as A_BNBWD does (coef = (mu, p, q)), so the data-gradient
+// GEMM need not store dz for this kernel.
+enum { W_PLAIN = 0, W_BNRELU = 1, W_UNSHUFFLE = 2, W_BNBWD = 3 };
 
 struct WgradArgs {
     DView a;
@@ -282,6 +285,8 @@ struct WgradArgs {
     int Q;
     int64_t M, mslice;
     float* slab;  // [S][P][Q]
+    const float* bz;     // W_BNBWD: raw z (same layout as b.src0)
+    const float* bcoef;  // W_BNBWD: (mu, p, q) x Q
 };
 
 template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
@@ -743,11 +748,18 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     const int bqq = tid % QQ, bmm = tid / QQ;
     const int q = q0 + 4 * bqq;
     const bool qv = q < g.Q;
-    float4 bsc = f4(1.f), bsh = f4(0.f);
-    if constexpr (BMODE == W_BNRELU) {
+    float4 bsc = f4(1.f), bsh = f4(0.f), bmu = f4(0.f), bp_ = f4(0.f), bq_ = f4(0.f);
+    if constexpr (BMODE == W_BNRELU || BMODE == W_BNBWD) {
         if (qv) {
             bsc = ld4(g.b.sc0 + q);
             bsh = ld4(g.b.sh0 + q);
+        }
+    }
+    if constexpr (BMODE == W_BNBWD) {
+        if (qv) {
+            bmu = ld4(g.bcoef + q);
+            bp_ = ld4(g.bcoef + g.Q + q);
+            bq_ = ld4(g.bcoef + 2 * g.Q + q);
         }
     }
 
@@ -782,6 +794,17 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
             if (qv && m < me) {
                 v = ld4(g.b.src0 + (int64_t)m * g.b.c0 + q);
                 if constexpr (BMODE == W_BNRELU) v = bnrelu4(v, bsc, bsh);
+                if constexpr (BMODE == W_BNBWD) {
+                    const float4 zz = ld4(g.bz + (int64_t)m * g.b.c0 + q);
+                    v.x = fmaf(zz.x, bsc.x, bsh.x) > 0.f ? v.x : 0.f;
+                    v.y = fmaf(zz.y, bsc.y, bsh.y) > 0.f ? v.y : 0.f;
+                    v.z = fmaf(zz.z, bsc.z, bsh.z) > 0.f ? v.z : 0.f;
+                    v.w = fmaf(zz.w, bsc.w, bsh.w) > 0.f ? v.w : 0.f;
+                    v.x = bsc.x * (v.x - bp_.x - (zz.x - bmu.x) * bq_.x);
+                    v.y = bsc.y * (v.y - bp_.y - (zz.y - bmu.y) * bq_.y);
+                    v.z = bsc.z * (v.z - bp_.z - (zz.z - bmu.z) * bq_.z);
+                    v.w = bsc.w * (v.w - bp_.w - (zz.w - bmu.w) * bq_.w);
+                }
                 if constexpr (BDROP) {
                     const uint64_t i = (uint64_t)m * g.b.C + q;
                     v = mul4(v, drop_mult4(g.b.seed, i, g.b.rate, g.b.inv_keep));
@@ -939,7 +962,7 @@ void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
     const bool vec = a.P % 4 == 0 && a.Q % 4 == 0 && (AMODE != W_UNSHUFFLE || a.uf % 4 == 0) &&
                      (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
                      ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
-    if (vec) {
+    if (vec || BMODE == W_BNBWD) {
         if (w.bp == 128 && w.bq == 128)
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
         else if (w.bp == 128)
@@ -950,7 +973,8 @@ void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
             gemm_wgrad_vec<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
         return;
     }
-    if (w.bp == 128 && w.bq == 128)
+    if constexpr (BMODE == W_BNBWD) return;  // (unreachable: the vectorised kernel above)
+    else if (w.bp == 128 && w.bq == 128)
         gemm_wgrad_kernel<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
     else if (w.bp == 128)
         gemm_wgrad_kernel<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
@@ -981,6 +1005,8 @@ int run_wgrad(WgradArgs a, int amode, int bmode, float* out, void* ws, size_t ws
             launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, true>(a, w, st);
         else
             launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, false>(a, w, st);
+    } else if (amode == W_PLAIN && bmode == W_BNBWD) {
+        launch_wgrad_t<W_PLAIN, false, W_BNBWD, false>(a, w, st);
     } else if (amode == W_BNRELU && bmode == W_PLAIN) {
         if (ad)
             launch_wgrad_t<W_BNRELU, true, W_PLAIN, false>(a, w, st);
@@ -1108,6 +1134,27 @@ extern "C" int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_
     a.Q = cout;
     a.M = m;
     return run_wgrad(a, W_PLAIN, W_PLAIN, d_pw_kernel, ws, ws_bytes, as_stream(stream), "unet_pointwise_bwd_filter");
+}
+
+extern "C" int unet_pointwise_bwd_filter_bnrelu(const float* y, const float* da, const float* z, int64_t m, int cin,
+                                                int cout, const float* scale, const float* shift, const float* coef,
+                                                float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    const char* op = "unet_pointwise_bwd_filter_bnrelu";
+    UNET_CHECK_ARG(y && da && z && scale && shift && coef && d_pw_kernel, "%s: null pointer", op);
+    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0, "%s: bad sizes", op);
+    UNET_CHECK_ARG(((uintptr_t)y | (uintptr_t)da | (uintptr_t)z | (uintptr_t)scale | (uintptr_t)shift |
+                    (uintptr_t)coef) % 16 == 0, "%s: operands must be 16-B aligned", op);
+    WgradArgs a{};
+    a.a = plain_view(y, cin);
+    a.P = cin;
+    a.b = plain_view(da, cout);
+    a.b.sc0 = scale;
+    a.b.sh0 = shift;
+    a.bz = z;
+    a.bcoef = coef;
+    a.Q = cout;
+    a.M = m;
+    return run_wgrad(a, W_PLAIN, W_BNBWD, d_pw_kernel, ws, ws_bytes, as_stream(stream), op);
 }
 
 // ------------------------------------------------------------ transposed conv 2x2/2 ----

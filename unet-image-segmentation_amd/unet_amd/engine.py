@@ -147,6 +147,11 @@ class UNetEngine:
         # BN-backward statistics of a block emitted by the launch that completes its da (the next
         # block's depthwise data gradient through BN+ReLU or the max-pool), not by a pass over (da, z)
         self.fuse_bn_stats = os.environ.get("UNET_FUSE_BN_STATS", "1") != "0"
+        # the pointwise weight gradient forms dz from (da, z) itself, so the data-gradient GEMM on the
+        # critical path does not store dz (its HBM write moves to a read on the side stream).  Off:
+        # measured 3 % slower (1231 vs 1269 img/s, r1w) -- the two streams share HBM, so moving bytes
+        # between them does not shorten the step; only removing bytes does.
+        self.wgrad_forms_dz = os.environ.get("UNET_WGRAD_DZ", "0") != "0"
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -396,16 +401,21 @@ class UNetEngine:
                 ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
+            wdz = self.wgrad_forms_dz and drop_rate == 0.0
             ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef, drop_rate,
-                                          drop_seed, dy, dz)
+                                          drop_seed, dy, None if wdz else dz)
         else:
+            wdz = False
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gdk, gpk = self._gwts(b)
 
         def weight_grads():
-            ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
+            if wdz:
+                ops.pointwise_bwd_filter_bnrelu(bb.y, bb.da, bb.z, m, b.cin, b.cout, bb.scale, bb.shift, bb.coef, gpk)
+            else:
+                ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
             ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])

@@ -267,6 +267,20 @@ def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
           _ptr(dz), m, cin, cout, _ptr(dpk), ws, wsb, _stream())
 
 
+def pointwise_bwd_filter_bnrelu(y: Tensor, da: Tensor, z: Tensor, m: int, cin: int, cout: int, scale: Tensor,
+                                shift: Tensor, coef: Tensor, dpk: Tensor):
+    """pointwise_bwd_filter with dz formed on load from (da, z) and the BN-backward coefficients."""
+    _check(y, "y", m * cin)
+    _check(da, "da", m * cout)
+    _check(z, "z", m * cout)
+    _check(coef, "coef", 3 * cout)
+    _check(dpk, "d_pointwise_kernel", cin * cout)
+    ws, wsb = _ws(L.query("unet_pointwise_bwd_filter_workspace", m, cin, cout), y.device)
+    _call("unet_pointwise_bwd_filter_bnrelu", (2.0 * m * cin * cout, 4.0 * (m * cin + 2 * m * cout + cin * cout)),
+          _ptr(y), _ptr(da), _ptr(z), m, cin, cout, _ptr(scale), _ptr(shift), _ptr(coef), _ptr(dpk), ws, wsb,
+          _stream())
+
+
 def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
     vs = x.c_struct()
     return bool(L.load().unet_sepconv_fwd_supported(ctypes.byref(vs), n, h, w, cout))
