@@ -108,6 +108,20 @@ int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w,
                                     const float* rstd, float* bn_partials,
                                     unet_stream_t stream);
 
+/* Data and filter gradient in one pass over dy (dy read once): dx0/dx1 as
+ * unet_dwconv3x3_bwd_data (dx0 may be NULL for PLAIN/BNRELU views: filter only),
+ * d_dw_kernel as unet_dwconv3x3_bwd_filter (workspace: _bwd_workspace), and with
+ * bn_partials != NULL (BNRELU / POOL_BNRELU views) the view block's
+ * BatchNorm-backward partials as unet_dwconv3x3_bwd_data_bnstats, over
+ * S = unet_dwconv3x3_bwd_slabs(...) slabs (0: no such path for this shape).  */
+int unet_dwconv3x3_bwd_slabs(const unet_view* x, int n, int h, int w);
+size_t unet_dwconv3x3_bwd_workspace(int n, int h, int w, int c);
+int unet_dwconv3x3_bwd(const unet_view* x, int n, int h, int w,
+                       const float* dw_kernel, const float* dy, float* dx0,
+                       float* dx1, float* d_dw_kernel, const float* mean,
+                       const float* rstd, float* bn_partials, void* ws,
+                       size_t ws_bytes, unet_stream_t stream);
+
 size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c);
 /* d_dw_kernel (3,3,C,1) = sum over pixels of x(shifted) * dy (overwrites). */
 int unet_dwconv3x3_bwd_filter(const unet_view* x, int n, int h, int w,

@@ -152,6 +152,10 @@ class UNetEngine:
         # measured 3 % slower (1231 vs 1269 img/s, r1w) -- the two streams share HBM, so moving bytes
         # between them does not shorten the step; only removing bytes does.
         self.wgrad_forms_dz = os.environ.get("UNET_WGRAD_DZ", "0") != "0"
+        # depthwise data + filter gradient in one pass over dy (unet_dwconv3x3_bwd) on the main stream.
+        # Off: it saves one dy read but moves the filter work onto the critical path; measured
+        # 1245 vs 1258 img/s (r1x)
+        self.fuse_dw_bwd = os.environ.get("UNET_FUSE_DW_BWD", "0") != "0"
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -411,12 +415,16 @@ class UNetEngine:
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gdk, gpk = self._gwts(b)
 
+        fused_dw = (self.fuse_dw_bwd and dx0 is not None and not b.wcin
+                    and ops.dwconv3x3_bwd_slabs(view_in, n, h, w) > 0)
+
         def weight_grads():
             if wdz:
                 ops.pointwise_bwd_filter_bnrelu(bb.y, bb.da, bb.z, m, b.cin, b.cout, bb.scale, bb.shift, bb.coef, gpk)
             else:
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+            if not fused_dw:
+                ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
                 self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
@@ -427,7 +435,19 @@ class UNetEngine:
                 weight_grads()
         else:
             weight_grads()
-        if dx0 is not None:
+        if fused_dw:
+            S = ops.dwconv3x3_bwd_slabs(view_in, n, h, w)
+            tb = stats_target if (stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd) else None
+            if tb is not None:
+                need = ops.bn_stats_partials_numel(S, view_in.channels)
+                if tb.bnpart is None or tb.bnpart.numel() < need:
+                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                ops.dwconv3x3_bwd(view_in, n, h, w, dk, dy, dx0, dx1, gdk, tb.mean if self.use_bn else None,
+                                  tb.rstd if self.use_bn else None, tb.bnpart)
+                tb.bn_slabs = S
+            else:
+                ops.dwconv3x3_bwd(view_in, n, h, w, dk, dy, dx0, dx1, gdk)
+        elif dx0 is not None:
             S = 0
             if stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
                 S = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w)

@@ -226,6 +226,29 @@ def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Te
           _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
 
 
+def dwconv3x3_bwd_slabs(x: View, n, h, w) -> int:
+    """Slab count of dwconv3x3_bwd's BN partials (0: no fused data + filter path for this shape)."""
+    vs = x.c_struct()
+    return L.query("unet_dwconv3x3_bwd_slabs", ctypes.byref(vs), n, h, w)
+
+
+def dwconv3x3_bwd(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Optional[Tensor], dx1: Optional[Tensor],
+                  ddk: Tensor, mean=None, rstd=None, partials: Optional[Tensor] = None):
+    """Depthwise data + filter gradient in one pass over dy (+ the view block's BN partials)."""
+    C = x.channels
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(dy, "dy", n * h * w * C)
+    _check(ddk, "d_depthwise_kernel", 9 * C)
+    if partials is not None:
+        _check(partials, "bn_partials", bn_stats_partials_numel(dwconv3x3_bwd_slabs(x, n, h, w), C))
+    ws, wsb = _ws(L.query("unet_dwconv3x3_bwd_workspace", n, h, w, C), dy.device)
+    vs = x.c_struct()
+    m = n * h * w
+    nb = 2 * x.src_bytes(n, h, w) + 8.0 * m * C
+    _call("unet_dwconv3x3_bwd", (36.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dx0),
+          _ptr(dx1), _ptr(ddk), _ptr(mean), _ptr(rstd), _ptr(partials), ws, wsb, _stream())
+
+
 def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
     C = x.channels
     _check(dy, "dy", n * h * w * C)
