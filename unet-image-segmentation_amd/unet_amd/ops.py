@@ -221,7 +221,8 @@ def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Te
     _check(partials, "bn_partials", bn_stats_partials_numel(S, C))
     vs = x.c_struct()
     m = n * h * w
-    nb = 8.0 * m * C + 3.0 * x.src_bytes(n, h, w) + 4.0 * S * 2 * C
+    # read dy, write dx; pool: the 2x2 sources and the read-modify-write of dx0; BN+ReLU: z once
+    nb = 8.0 * m * C + (3.0 * x.src_bytes(n, h, w) if x.mode == L.VIEW_POOL_BNRELU else 4.0 * m * C) + 4.0 * S * 2 * C
     _call("unet_dwconv3x3_bwd_data_bnstats", (18.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy),
           _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
 
