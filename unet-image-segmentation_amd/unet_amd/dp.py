@@ -38,6 +38,11 @@ def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("UNET_DP_ONE_DEVICE") == "1":
+        # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo
+        # collectives (RCCL refuses two ranks on one GPU)
+        local = 0
+        backend = backend or "gloo"
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
