@@ -156,6 +156,9 @@ class UNetEngine:
         # Off: it saves one dy read but moves the filter work onto the critical path; measured
         # 1245 vs 1258 img/s (r1x)
         self.fuse_dw_bwd = os.environ.get("UNET_FUSE_DW_BWD", "0") != "0"
+        # 256x256 level: run the data-gradient GEMM and the depthwise data gradient in batch chunks,
+        # interleaved, so each chunk's dy is consumed while it is still in the Infinity Cache
+        self.l0_chunks = int(os.environ.get("UNET_L0_CHUNKS", "1"))
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -406,10 +409,18 @@ class UNetEngine:
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
             wdz = self.wgrad_forms_dz and drop_rate == 0.0
-            ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef, drop_rate,
-                                          drop_seed, dy, None if wdz else dz)
+            chunked = (self.l0_chunks > 1 and b.level == 0 and dx0 is not None and not wdz and drop_rate == 0.0
+                       and view_in.drop_rate == 0.0 and n % self.l0_chunks == 0 and not self.fuse_dw_bwd)
+            if chunked:  # chunk 0 only; the others are interleaved with the depthwise data gradient below
+                nc = n // self.l0_chunks
+                ops.pointwise_bwd_data_bnrelu(bb.da[:nc], bb.z[:nc], nc * h * w, b.cin, b.cout, pk, bb.scale,
+                                              bb.shift, bb.coef, 0.0, 0, dy.view(n, h, w, b.cin)[:nc],
+                                              dz.view(n, h, w, b.cout)[:nc])
+            else:
+                ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
+                                              drop_rate, drop_seed, dy, None if wdz else dz)
         else:
-            wdz = False
+            wdz = chunked = False
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
@@ -429,13 +440,45 @@ class UNetEngine:
                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
                 self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
 
-        if self.overlap:  # weight gradients off the critical path, on the side stream
-            self.side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self.side):
+        if not chunked:  # (chunked: after all chunks' data gradients, below)
+            if self.overlap:  # weight gradients off the critical path, on the side stream
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    weight_grads()
+            else:
                 weight_grads()
-        else:
-            weight_grads()
-        if fused_dw:
+        if chunked:
+            K = self.l0_chunks
+            nc, mc = n // K, (n // K) * h * w
+            dy4, dz4 = dy.view(n, h, w, b.cin), dz.view(n, h, w, b.cout)
+            tb = stats_target if (stats_target is not None and self.fuse_bn_stats) else None
+            Sc = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in.batch(slice(0, nc)), nc, h, w) if tb is not None else 0
+            if Sc > 0:
+                need = ops.bn_stats_partials_numel(K * Sc, view_in.channels)
+                if tb.bnpart is None or tb.bnpart.numel() < need:
+                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+            for c in range(K):
+                sl = slice(c * nc, (c + 1) * nc)
+                if c > 0:  # chunk 0's data gradient was issued before the side-stream fork
+                    ops.pointwise_bwd_data_bnrelu(bb.da[sl], bb.z[sl], mc, b.cin, b.cout, pk, bb.scale, bb.shift,
+                                                  bb.coef, 0.0, 0, dy4[sl], dz4[sl])
+                sub = view_in.batch(sl)
+                if Sc > 0:
+                    ops.dwconv3x3_bwd_data_bnstats(sub, nc, h, w, dk, dy4[sl], dx0[sl],
+                                                   tb.mean if self.use_bn else None,
+                                                   tb.rstd if self.use_bn else None,
+                                                   tb.bnpart[c * Sc * 2 * view_in.channels:][:ops.bn_stats_partials_numel(Sc, view_in.channels)])
+                else:
+                    ops.dwconv3x3_bwd_data(sub, nc, h, w, dk, dy4[sl], dx0[sl], dx1[sl] if dx1 is not None else None)
+            if Sc > 0:
+                tb.bn_slabs = K * Sc
+            if self.overlap:
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    weight_grads()
+            else:
+                weight_grads()
+        elif fused_dw:
             S = ops.dwconv3x3_bwd_slabs(view_in, n, h, w)
             tb = stats_target if (stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd) else None
             if tb is not None:

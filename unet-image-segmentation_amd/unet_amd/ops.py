@@ -150,6 +150,13 @@ class View:
     def dropout(self, rate: float, seed: int) -> "View":
         return replace(self, drop_rate=float(rate), drop_seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
 
+    def batch(self, sl: slice) -> "View":
+        """The view of images sl of the batch (sources sliced along dim 0).  Not for dropout
+        views: the mask is drawn from the element's linear index in the whole batch."""
+        if self.drop_rate > 0.0:
+            raise ValueError("batch slices of a dropout view would draw a different mask")
+        return replace(self, src0=self.src0[sl], src1=self.src1[sl] if self.src1 is not None else None)
+
     def c_struct(self) -> UnetView:
         for name in ("src0", "scale0", "shift0", "src1", "scale1", "shift1"):
             t = getattr(self, name)
