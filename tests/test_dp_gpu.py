@@ -1,0 +1,34 @@
+"""Data-parallel train step on the GPU, two ranks (tools/dp_check.py under torch.distributed.run).
+On a one-GPU box both ranks share device 0 and gloo carries the collectives (RCCL refuses two
+ranks on one GPU); the engine's bucketed, hook-driven all-reduce and its deferred weight
+gradients are the same code the RCCL run uses.  Every rank must end the step with bitwise
+identical averaged gradients and weights."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_dp_two_ranks_consistent():
+    env = dict(os.environ)
+    if torch.cuda.device_count() < 2:
+        env["UNET_DP_ONE_DEVICE"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tools", "dp_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "identical across ranks: True" in r.stdout

@@ -159,6 +159,15 @@ class UNetEngine:
         # 256x256 level: run the data-gradient GEMM and the depthwise data gradient in batch chunks,
         # interleaved, so each chunk's dy is consumed while it is still in the Infinity Cache
         self.l0_chunks = int(os.environ.get("UNET_L0_CHUNKS", "1"))
+        # decoder levels whose weight gradients are deferred until the backward reaches the
+        # bottleneck: they are HBM-bound and then overlap the MFMA-bound deep levels instead of
+        # contending with the HBM-bound 256x256 / 128x128 data-gradient chain (measured 1272 ->
+        # 1296 img/s, r1za).  With all-reduce hooks the low-water mark is held back until the
+        # deferred work is issued, so buckets still complete from the end of the flat buffer.
+        dl = os.environ.get("UNET_DEFER_WGRAD", "0,1")
+        self.defer_wgrad_levels = {int(t) for t in dl.split(",") if t.strip()}
+        self._deferred: List = []
+        self._held_mark: Optional[int] = None
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -373,6 +382,9 @@ class UNetEngine:
         the hook (bucketed all-reduce) is issued from the side stream after it has caught up
         with the main stream."""
         if self.grad_hook is not None:
+            if self._deferred:  # gradients above this mark are not all issued yet: hold the mark
+                self._held_mark = self.train_layout.offsets[name]
+                return
             if self.overlap:
                 self.side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self.side):
@@ -440,7 +452,13 @@ class UNetEngine:
                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
                 self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
 
-        if not chunked:  # (chunked: after all chunks' data gradients, below)
+        defer = (self.overlap and b.name.startswith("dec")
+                 and b.level in self.defer_wgrad_levels and not chunked)
+        if defer:  # issued on the side stream later (_flush_deferred), after this point of main
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._deferred.append((ev, weight_grads))
+        elif not chunked:  # (chunked: after all chunks' data gradients, below)
             if self.overlap:  # weight gradients off the critical path, on the side stream
                 self.side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self.side):
@@ -506,6 +524,18 @@ class UNetEngine:
                 ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
+    def _flush_deferred(self):
+        for ev, fn in self._deferred:
+            self.side.wait_event(ev)
+            with torch.cuda.stream(self.side):
+                fn()
+        self._deferred = []
+        if self._held_mark is not None and self.grad_hook is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                self.grad_hook(self._held_mark)
+        self._held_mark = None
+
     def _view_of(self, A: Acts, b: Block) -> View:
         bb = A.blocks[b.name]
         return View.bnrelu(bb.z, bb.scale, bb.shift)
@@ -555,6 +585,7 @@ class UNetEngine:
                                       self.gvars[f"{stage}_upsample/bias"])
             self._grads_ready(f"{stage}_upsample/kernel")
         b1, b2 = self.bneck
+        self._flush_deferred()  # deferred decoder weight gradients overlap the deep levels
         self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da,
                         drop_rate=self.dropout_rate if drop else 0.0,
                         drop_seed=seeds["bneck_dropout"] if drop else 0, stats_target=A.blocks[b1.name])
@@ -569,6 +600,7 @@ class UNetEngine:
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
+        self._flush_deferred()
         if self.overlap:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
 
