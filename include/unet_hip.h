@@ -238,7 +238,8 @@ int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w,
 size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int cin,
                                             int cout);
 /* dx (n,h,w,Cin) = grad w.r.t. the view output (NULL: skip); dkernel, dbias
- * overwrite. */
+ * overwrite (both NULL: data gradient only, so the weight gradient can be a
+ * separate call with dx = NULL, e.g. on another stream). */
 int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w,
                                int cout, const float* kernel,
                                const float* dout, float* dx, float* dkernel,

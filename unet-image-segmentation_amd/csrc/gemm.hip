@@ -1204,8 +1204,9 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
     if (check_view(x, "unet_conv_transpose2x2_bwd")) return -1;
     UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
                    "unet_conv_transpose2x2_bwd: input view must be PLAIN or BNRELU");
-    UNET_CHECK_ARG(kernel && dout && dkernel && dbias && n > 0 && h > 0 && w > 0 && cout > 0,
-                   "unet_conv_transpose2x2_bwd: bad args");
+    UNET_CHECK_ARG(kernel && dout && n > 0 && h > 0 && w > 0 && cout > 0, "unet_conv_transpose2x2_bwd: bad args");
+    UNET_CHECK_ARG((dkernel == nullptr) == (dbias == nullptr) && (dx || dkernel),
+                   "unet_conv_transpose2x2_bwd: dkernel and dbias go together; nothing to compute");
     const int cin = x->c0;
     const int64_t M = (int64_t)n * h * w;
     UNET_CHECK_ARG(fits_i32(M, cin) && fits_i32(4 * M, cout), "unet_conv_transpose2x2_bwd: tensor too large");
@@ -1230,6 +1231,7 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
         int rc = launch_rows<A_UNSHUFFLE, false, E_STORE>(a, st, "unet_conv_transpose2x2_bwd(data)");
         if (rc) return rc;
     }
+    if (!dkernel) return 0;  // data gradient only
     // kernel gradient: dk[(a,b,co)][ci] = sum_m dU'[m, (a,b,co)] x[m, ci]
     WgradArgs wa{};
     wa.a = plain_view(dout, cout);

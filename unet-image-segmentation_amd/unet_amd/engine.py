@@ -166,6 +166,9 @@ class UNetEngine:
         # deferred work is issued, so buckets still complete from the end of the flat buffer.
         dl = os.environ.get("UNET_DEFER_WGRAD", "0,1")
         self.defer_wgrad_levels = {int(t) for t in dl.split(",") if t.strip()}
+        # Conv2DTranspose weight / bias gradients on the side stream (its data gradient stays on
+        # the critical path); the side stream is otherwise idle until the deferred work is issued
+        self.convt_wgrad_side = os.environ.get("UNET_CONVT_SIDE", "1") != "0"
         self._deferred: List = []
         self._held_mark: Optional[int] = None
 
@@ -580,9 +583,18 @@ class UNetEngine:
             if i == 0 and drop:
                 xv = xv.dropout(self.dropout_rate, seeds["bneck_dropout"])
             h, w = self._dims(b1.level + 1)
-            ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
-                                      A.blocks[prev.name].da, self.gvars[f"{stage}_upsample/kernel"],
-                                      self.gvars[f"{stage}_upsample/bias"])
+            gk, gb = self.gvars[f"{stage}_upsample/kernel"], self.gvars[f"{stage}_upsample/bias"]
+            if self.overlap and self.convt_wgrad_side:
+                # data gradient on the critical path, weight + bias gradients on the side stream
+                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
+                                          A.blocks[prev.name].da, None, None)
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
+                                              None, gk, gb)
+            else:
+                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
+                                          A.blocks[prev.name].da, gk, gb)
             self._grads_ready(f"{stage}_upsample/kernel")
         b1, b2 = self.bneck
         self._flush_deferred()  # deferred decoder weight gradients overlap the deep levels

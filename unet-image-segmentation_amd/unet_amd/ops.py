@@ -412,20 +412,23 @@ def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor]
           ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(b), _ptr(out), _stream())
 
 
-def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Optional[Tensor], dk: Tensor,
-                          db: Tensor):
+def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Optional[Tensor],
+                          dk: Optional[Tensor], db: Optional[Tensor]):
+    """Data gradient (dx) and/or weight + bias gradients (dk, db; both or neither)."""
     _check(dout, "dout", n * 4 * h * w * cout)
-    _check(dk, "dkernel", 4 * cout * x.c0)
-    _check(db, "dbias", cout)
+    if dk is not None:
+        _check(dk, "dkernel", 4 * cout * x.c0)
+        _check(db, "dbias", cout)
     if dx is not None:
         _check(dx, "dx", n * h * w * x.c0)
     ws, wsb = _ws(L.query("unet_conv_transpose2x2_bwd_workspace", n, h, w, x.c0, cout), dout.device)
     vs = x.c_struct()
     m = n * h * w
-    fl = (16.0 if dx is not None else 8.0) * m * x.c0 * cout  # dgrad + wgrad
-    nb = x.src_bytes(n, h, w) + 16.0 * m * cout + (4.0 * m * x.c0 if dx is not None else 0.0) + 32.0 * x.c0 * cout
-    _call("unet_conv_transpose2x2_bwd", (fl, nb), ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(dout), _ptr(dx), _ptr(dk),
-           _ptr(db), ws, wsb, _stream())
+    fl = ((8.0 if dx is not None else 0.0) + (8.0 if dk is not None else 0.0)) * m * x.c0 * cout
+    nb = ((16.0 * m * cout + 4.0 * m * x.c0 + 16.0 * x.c0 * cout if dx is not None else 0.0) +
+          (x.src_bytes(n, h, w) + 16.0 * m * cout + 16.0 * x.c0 * cout if dk is not None else 0.0))
+    _call("unet_conv_transpose2x2_bwd", (fl, nb), ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(dout), _ptr(dx),
+          _ptr(dk), _ptr(db), ws, wsb, _stream())
 
 
 # ---------------------------------------------------------------- head / loss ---
