@@ -602,7 +602,13 @@ TilePlan tile_plan(int N, int H, int W, int C) {
     return p;
 }
 int filter_blocks(const TilePlan& p) {
-    int g = (int)cdiv(1024, p.chunks);
+    static int target = -1;  // persistent blocks over all channel chunks (UNET_DWF_BLOCKS: tuning)
+    if (target < 0) {
+        const char* e = getenv("UNET_DWF_BLOCKS");
+        target = e ? atoi(e) : 1024;
+        if (target < 1) target = 1024;
+    }
+    int g = (int)cdiv(target, p.chunks);
     if (g > p.ntiles) g = p.ntiles;
     if (g < 1) g = 1;
     return g;

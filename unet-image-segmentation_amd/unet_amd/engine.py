@@ -527,12 +527,17 @@ class UNetEngine:
                 ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
-    def _flush_deferred(self):
-        for ev, fn in self._deferred:
+    def _flush_deferred(self, count: Optional[int] = None):
+        """Issue deferred weight-gradient work on the side stream: all of it, or `count` closures
+        (a few per block, so the host keeps the critical path's queue fed meanwhile)."""
+        k = len(self._deferred) if count is None else min(count, len(self._deferred))
+        for ev, fn in self._deferred[:k]:
             self.side.wait_event(ev)
             with torch.cuda.stream(self.side):
                 fn()
-        self._deferred = []
+        self._deferred = self._deferred[k:]
+        if self._deferred:
+            return
         if self._held_mark is not None and self.grad_hook is not None:
             self.side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.side):
@@ -597,7 +602,8 @@ class UNetEngine:
                                           A.blocks[prev.name].da, gk, gb)
             self._grads_ready(f"{stage}_upsample/kernel")
         b1, b2 = self.bneck
-        self._flush_deferred()  # deferred decoder weight gradients overlap the deep levels
+        self._flush_deferred()  # deferred decoder weight gradients overlap the deep levels (all at once:
+        # issuing them a few per block measured slower, 1278 vs 1301 img/s)
         self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da,
                         drop_rate=self.dropout_rate if drop else 0.0,
                         drop_seed=seeds["bneck_dropout"] if drop else 0, stats_target=A.blocks[b1.name])
