@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 2
+#define UNET_ABI_VERSION 3
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -206,9 +206,12 @@ int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c,
                            float* dbeta, float* coef, void* ws, size_t ws_bytes,
                            unet_stream_t stream);
 /* Finish of the statistics from S producer-side partial slabs ([S][2][c],
- * fixed-order double reduction): the outputs of unet_bn_relu_bwd_stats.  The
- * partials buffer holds unet_bn_stats_partials_size(S, c) bytes: the slabs,
- * then scratch for the first pass of large slab counts.                      */
+ * fixed-order double reduction): the outputs of unet_bn_relu_bwd_stats, in one
+ * launch (64-slab chunk sums; the last block of each channel range to finish
+ * sums the chunk rows).  The partials buffer holds
+ * unet_bn_stats_partials_size(S, c) bytes: the slabs, the chunk rows, then
+ * ceil(c/64) arrival counters that must be zero before the first call --
+ * allocate the buffer zeroed once; every call leaves them zero again.        */
 size_t unet_bn_stats_partials_size(int S, int c);
 int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, int c,
                                   const float* mean, const float* rstd,

@@ -42,6 +42,10 @@ def test_workspace_queries():
     # ceil(1000/128) tiles x C x float2 (256-B aligned) + one chunk record x C x double2 of finalize scratch
     assert q("unet_bn_partials_size", 1000, 64) == 8 * 64 * 8 + 1 * 64 * 16
     assert q("unet_bn_partials_size", 0, 64) == 0
+    # BN-backward slabs [S][2C] float | double chunk rows, one per 64 slabs | ceil(C/64) counters
+    assert q("unet_bn_stats_partials_size", 300, 64) == 300 * 128 * 4 + 5 * 128 * 8 + 1 * 4
+    assert q("unet_bn_stats_partials_size", 1, 8) == 256 + 256 + 1 * 4
+    assert q("unet_bn_stats_partials_size", 100, 1024) == 100 * 2048 * 4 + 2 * 2048 * 8 + 16 * 4
     for fn, args in [("unet_dwconv3x3_bwd_filter_workspace", (16, 256, 256, 64)),
                      ("unet_pointwise_bwd_filter_workspace", (16 * 65536, 64, 64)),
                      ("unet_bn_relu_bwd_workspace", (16 * 65536, 64)),

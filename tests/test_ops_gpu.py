@@ -421,7 +421,7 @@ def test_dwconv_bwd_data_bnstats(ops, mode, use_bn, n, h, w, c):
     assert S > 0
     mean = dev(f32(rng.standard_normal(c) * 0.1))
     rstd = dev(f32(1.0 + rng.random(c)))
-    part = torch.empty(ops.bn_stats_partials_numel(S, c), device="cuda")
+    part = torch.zeros(ops.bn_stats_partials_numel(S, c), device="cuda")  # counters zero
     dx_f, dx_p = dev(init), dev(init)
     ops.dwconv3x3_bwd_data_bnstats(v, n, h, w, dk, dy, dx_f, mean if use_bn else None, rstd if use_bn else None,
                                    part)
@@ -432,8 +432,12 @@ def test_dwconv_bwd_data_bnstats(ops, mode, use_bn, n, h, w, c):
     for fused in (True, False):
         dg, db, coef = (torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"),
                         torch.empty(3 * c, device="cuda"))
-        if fused:
+        if fused:  # twice: the arrival counters are left zero, the result is deterministic
             ops.bn_relu_bwd_stats_finish(part, S, m, c, mean, rstd, use_bn, dg if use_bn else None, db, coef)
+            first = coef.clone()
+            ops.bn_relu_bwd_stats_finish(part, S, m, c, mean, rstd, use_bn, dg if use_bn else None, db, coef)
+            assert torch.equal(first, coef)
+            assert not torch.any(part[-((c + 63) // 64):].view(torch.int32))
         else:
             ops.bn_relu_bwd_stats(dx_p, t["src0"], m, c, mean, rstd, t["sc0"], t["sh0"], use_bn, 0.0, 0,
                                   dg if use_bn else None, db, coef)
@@ -469,7 +473,7 @@ def test_head_bwd_bnstats(ops, use_bn, loss_kind):
     assert S > 0
     mean = dev(f32(rng.standard_normal(c) * 0.1))
     rstd = dev(f32(1.0 + rng.random(c)))
-    part = torch.empty(ops.bn_stats_partials_numel(S, c), device="cuda")
+    part = torch.zeros(ops.bn_stats_partials_numel(S, c), device="cuda")  # counters zero
     outs = []
     for fused in (True, False):
         dx, dk, db = torch.empty((n, h, w, c), device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
@@ -517,7 +521,7 @@ def test_dwconv_bwd_fused(ops, mode, n, h, w, c0, c1, drop):
     ga, gb = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((3, 3, C, 1), device="cuda")
     stats = mode in (1, 2)
     S = ops.dwconv3x3_bwd_slabs(v, n, h, w)
-    part = torch.empty(ops.bn_stats_partials_numel(S, C), device="cuda") if stats else None
+    part = torch.zeros(ops.bn_stats_partials_numel(S, C), device="cuda") if stats else None
     mean = dev(f32(rng.standard_normal(C) * 0.1))
     rstd = dev(f32(1.0 + rng.random(C)))
     ops.dwconv3x3_bwd(v, n, h, w, dk, dy, dx0a, dx1a, ga, mean if stats else None, rstd if stats else None, part)

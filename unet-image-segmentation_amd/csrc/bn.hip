@@ -8,6 +8,7 @@
 // Backward is two passes over (da, z): per-channel sums (g, g*xhat) then the elementwise
 // dz, with the ReLU mask and the consumer's dropout mask recomputed, not stored.
 #include "view.h"
+#include "lastblock.h"
 
 namespace unet {
 
@@ -143,7 +144,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const float* __restrict__ rstd,
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             float rate, float inv_keep, uint64_t seed, int CT,
-                                                            int64_t rpc, float* __restrict__ part) {
+                                                            int64_t rpc, float* __restrict__ part,
+                                                            unsigned* __restrict__ cnt = nullptr, int ncnt = 0) {
+    if (cnt && blockIdx.x == 0 && blockIdx.y == 0)  // the statistics launch that follows counts on them
+        for (int i = threadIdx.x; i < ncnt; i += blockDim.x) cnt[i] = 0u;
     const int CQ = VEC ? C / 4 : C;
     const int PL = 256 / CT;
     const int tid = threadIdx.x, cl = tid % CT, pl = tid / CT;
@@ -287,88 +291,126 @@ __global__ void bn_bwd_coef_kernel(const float* sums, int C, int64_t M, int use_
 }
 
 // Statistics-only finish: the fixed-order slab reduction of (S1, S2) fused with the coefficient
-// kernel above.  Block = 16 channel quads x 32 slab groups; group g sums slabs g, g+32, ... in
-// double, then a fixed-order tree over the groups (same order as reduce_tall4).  T = float for
-// producer slabs, double for the chunk sums of bn_bwd_chunk_kernel (large slab counts).
-template <typename T>
-__device__ __forceinline__ void load_quad(const T* p, double* a) {
-    if constexpr (sizeof(T) == 4) {
-        const float4 u = ld4(p);
-        a[0] += (double)u.x; a[1] += (double)u.y; a[2] += (double)u.z; a[3] += (double)u.w;
-    } else {
-        const double2 u = *reinterpret_cast<const double2*>(p), v = *reinterpret_cast<const double2*>(p + 2);
-        a[0] += u.x; a[1] += u.y; a[2] += v.x; a[3] += v.y;
-    }
-}
-template <int LQ, int G>
-__device__ __forceinline__ void tree_reduce8(double (*red)[G * LQ], double* a) {
-    const int g = threadIdx.x / LQ;
+// kernel above, in ONE launch.  Block (x, y) = 16 channel quads x 16 slab groups over slabs
+// [64 y, 64 y + 64) (all S slabs when the grid has one row); groups are combined by wave shuffles
+// and a 4-wave LDS step (4 KB of LDS: the block still fits beside side-stream GEMM blocks that
+// hold most of a CU's LDS -- the 32 KB version waited up to 140 us for a slot, r1zd).  With
+// several rows each block publishes its chunk row (double) and the last block of column x to
+// arrive (lastblock.h) sums the rows in order and writes dgamma / dbeta / coef.
+constexpr int kLQ = 16, kSG = 16;
+__device__ __forceinline__ void group_reduce8(double* a, double (*red)[8][kLQ]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[k][threadIdx.x] = a[k];
+    for (int k = 0; k < 8; ++k) {
+        a[k] += __shfl_xor(a[k], 16);
+        a[k] += __shfl_xor(a[k], 32);
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane < kLQ) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[w][k][lane] = a[k];
+    }
     __syncthreads();
-    for (int half = G / 2; half > 0; half >>= 1) {
-        if (g < half) {
+    if (threadIdx.x < kLQ) {
+        const int t = threadIdx.x;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + half * LQ];
-        }
-        __syncthreads();
+        for (int k = 0; k < 8; ++k) a[k] = ((red[0][k][t] + red[1][k][t]) + red[2][k][t]) + red[3][k][t];
     }
 }
-constexpr int kFinChunk = 256;  // slabs per block of the first pass
-// First pass for many slabs: block (x, y) sums slabs [256 y, 256 y + 256) of its 16 channel quads
-// (32 groups x 8 slabs, fixed order) into chunk row y (double).
-__global__ __launch_bounds__(512) void bn_bwd_chunk_kernel(const float* __restrict__ part, int S, int C,
-                                                           double* __restrict__ chunks) {
-    constexpr int LQ = 16, G = 32;
-    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
-    const int c = (blockIdx.x * LQ + q) * 4;
-    const int s0 = blockIdx.y * kFinChunk, s1 = s0 + kFinChunk < S ? s0 + kFinChunk : S;
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restrict__ part, int S, int C, int64_t M,
+                                                           int use_bn, const float* mean, const float* rstd,
+                                                           float* dgamma, float* dbeta, float* coef,
+                                                           double* chunks, unsigned* cnt) {
+    const int q = threadIdx.x % kLQ, g = threadIdx.x / kLQ;
+    const int c = (blockIdx.x * kLQ + q) * 4;
+    const int nch = gridDim.y;
+    const int s0 = blockIdx.y * kGroupSlabs, s1 = nch == 1 || s0 + kGroupSlabs > S ? S : s0 + kGroupSlabs;
+    __shared__ double red[4][8][kLQ];
+    __shared__ int flag;
     double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (c < C) {
-#pragma unroll 4
-        for (int s = s0 + g; s < s1; s += G) {
-            load_quad(part + (int64_t)s * 2 * C + c, a);
-            load_quad(part + (int64_t)s * 2 * C + C + c, a + 4);
-        }
-    }
-    __shared__ double red[8][G * LQ];
-    tree_reduce8<LQ, G>(red, a);
-    if (g != 0 || c >= C) return;
-    double* out = chunks + (int64_t)blockIdx.y * 2 * C;
+        int s = s0 + g;
+        for (; s + 3 * kSG < s1; s += 4 * kSG) {  // 8 loads in flight
+            float4 u[4], v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        out[c + k] = red[k][q];
-        out[C + c + k] = red[4 + k][q];
-    }
-}
-template <typename T>
-__global__ __launch_bounds__(512) void bn_bwd_finish_kernel(const T* __restrict__ part, int S, int C, int64_t M,
-                                                            int use_bn, const float* mean, const float* rstd,
-                                                            float* dgamma, float* dbeta, float* coef) {
-    constexpr int LQ = 16, G = 32;
-    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
-    const int c = (blockIdx.x * LQ + q) * 4;
-    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (c < C) {
-        for (int s = g; s < S; s += G) {
-            load_quad(part + (int64_t)s * 2 * C + c, a);
-            load_quad(part + (int64_t)s * 2 * C + C + c, a + 4);
+            for (int k = 0; k < 4; ++k) {
+                u[k] = ld4(part + (int64_t)(s + k * kSG) * 2 * C + c);
+                v[k] = ld4(part + (int64_t)(s + k * kSG) * 2 * C + C + c);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[0] += (double)u[k].x; a[1] += (double)u[k].y; a[2] += (double)u[k].z; a[3] += (double)u[k].w;
+                a[4] += (double)v[k].x; a[5] += (double)v[k].y; a[6] += (double)v[k].z; a[7] += (double)v[k].w;
+            }
+        }
+        for (; s < s1; s += kSG) {
+            const float4 u = ld4(part + (int64_t)s * 2 * C + c), v = ld4(part + (int64_t)s * 2 * C + C + c);
+            a[0] += (double)u.x; a[1] += (double)u.y; a[2] += (double)u.z; a[3] += (double)u.w;
+            a[4] += (double)v.x; a[5] += (double)v.y; a[6] += (double)v.z; a[7] += (double)v.w;
         }
     }
-    __shared__ double red[8][G * LQ];
-    tree_reduce8<LQ, G>(red, a);
-    if (g != 0 || c >= C) return;
+    group_reduce8(a, red);
+    if (nch > 1) {
+        if (threadIdx.x < kLQ && c < C) {
+            double* row = chunks + (int64_t)blockIdx.y * 2 * C;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                st_agent(row + c + k, a[k]);
+                st_agent(row + C + c + k, a[4 + k]);
+            }
+        }
+        if (!last_arrival(cnt + blockIdx.x, (unsigned)nch, &flag)) return;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = 0.0;
+        if (c < C) {
+            int r = g;
+            for (; r + kSG < nch; r += 2 * kSG) {
+                double u[2][8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        u[h][k] = ld_agent(chunks + (int64_t)(r + h * kSG) * 2 * C + c + k);
+                        u[h][4 + k] = ld_agent(chunks + (int64_t)(r + h * kSG) * 2 * C + C + c + k);
+                    }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) a[k] += u[h][k];
+            }
+            for (; r < nch; r += kSG)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a[k] += ld_agent(chunks + (int64_t)r * 2 * C + c + k);
+                    a[4 + k] += ld_agent(chunks + (int64_t)r * 2 * C + C + c + k);
+                }
+        }
+        group_reduce8(a, red);
+    }
+    if (threadIdx.x >= kLQ || c >= C) return;
     const float invM = 1.0f / (float)M;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int cc = c + k;
-        const float s1 = (float)red[k][q], s2 = (float)red[4 + k][q];
-        if (dbeta) dbeta[cc] = s1;
-        if (use_bn && dgamma) dgamma[cc] = s2;
+        const float s1v = (float)a[k], s2v = (float)a[4 + k];
+        if (dbeta) dbeta[cc] = s1v;
+        if (use_bn && dgamma) dgamma[cc] = s2v;
         coef[cc] = use_bn ? mean[cc] : 0.f;
-        coef[C + cc] = use_bn ? s1 * invM : 0.f;
-        coef[2 * C + cc] = use_bn ? rstd[cc] * (s2 * invM) : 0.f;
+        coef[C + cc] = use_bn ? s1v * invM : 0.f;
+        coef[2 * C + cc] = use_bn ? rstd[cc] * (s2v * invM) : 0.f;
     }
+}
+
+// dgamma / dbeta / coef from S slabs [S][2c] (c % 4 == 0) in one launch; with more than 64 slabs
+// it needs `scratch` (cdiv(S, 64) x 2c doubles) and cdiv(c, 64) counters that are zero on entry
+// (left zero on exit).
+int bwd_stats_finish(const float* part, int S, int c, int64_t m, int use_bn, const float* mean, const float* rstd,
+                     float* dgamma, float* dbeta, float* coef, double* scratch, unsigned* cnt, hipStream_t st) {
+    const unsigned gx = (unsigned)cdiv(c / 4, kLQ);
+    const unsigned nch = S <= kGroupSlabs ? 1u : (unsigned)cdiv(S, kGroupSlabs);
+    bn_bwd_stats_kernel<<<dim3(gx, nch), 256, 0, st>>>(part, S, c, m, use_bn, mean, rstd, dgamma, dbeta, coef, scratch,
+                                                       cnt);
+    UNET_CHECK_LAUNCH("bn backward statistics (finish)");
+    return 0;
 }
 
 template <bool VEC>
@@ -474,7 +516,9 @@ extern "C" int unet_bn_infer_params(const float* gamma, const float* beta, const
 extern "C" size_t unet_bn_relu_bwd_workspace(int64_t m, int c) {
     if (m <= 0 || c <= 0) return 0;
     RedPlan p = red_plan(m, c);
-    return align_up((size_t)p.chunks * 2 * c * sizeof(float), 256) + align_up((size_t)2 * c * sizeof(float), 256);
+    return align_up((size_t)p.chunks * 2 * c * sizeof(float), 256) + align_up((size_t)2 * c * sizeof(float), 256) +
+           align_up((size_t)cdiv(p.chunks, kGroupSlabs) * 2 * c * sizeof(double), 256) +  // finish scratch
+           align_up((size_t)cdiv(c, 64) * sizeof(unsigned), 256);  // finish counters (zeroed by the reduce launch)
 }
 
 namespace {
@@ -497,10 +541,16 @@ int bn_relu_bwd_impl(const float* da, const float* z, int64_t m, int c, const fl
     const float inv_keep = drop_rate > 0.f ? 1.0f / (1.0f - drop_rate) : 1.0f;
     const bool vec = c % 4 == 0;
     const bool drop = drop_rate > 0.f;
+    const bool stats_only = coef_out && vec;  // reduce + one statistics launch (bwd_stats_finish)
+    double* scratch = reinterpret_cast<double*>(reinterpret_cast<char*>(sums) +
+                                                align_up((size_t)2 * c * sizeof(float), 256));
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(scratch) +
+                                                align_up((size_t)cdiv(p.chunks, kGroupSlabs) * 2 * c * sizeof(double), 256));
+    const int ncnt = stats_only ? (int)cdiv(c, 64) : 0;
     dim3 grid(p.ctiles, (unsigned)p.chunks);
 #define UNET_BNB(D, V)                                                                                        \
     bn_bwd_reduce_kernel<D, V><<<grid, 256, 0, st>>>(da, z, m, c, mu, rs, scale, shift, drop_rate, inv_keep, \
-                                                     drop_seed, p.CT, p.rpc, part)
+                                                     drop_seed, p.CT, p.rpc, part, ncnt ? cnt : nullptr, ncnt)
     if (drop) {
         if (vec) UNET_BNB(true, true);
         else UNET_BNB(true, false);
@@ -510,12 +560,9 @@ int bn_relu_bwd_impl(const float* da, const float* z, int64_t m, int c, const fl
     }
 #undef UNET_BNB
     UNET_CHECK_LAUNCH("unet_bn_relu_bwd(reduce)");
-    if (coef_out && vec) {  // statistics-only entry (unet_bn_relu_bwd_stats): reduce + coefficients
-        bn_bwd_finish_kernel<float><<<(unsigned)cdiv(c / 4, 16), 512, 0, st>>>(part, (int)p.chunks, c, m, use_bn, mean, rstd,
-                                                                        dgamma, dbeta, coef_out);
-        UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats(finish)");
-        return 0;
-    }
+    if (stats_only)  // statistics-only entry (unet_bn_relu_bwd_stats): reduce + coefficients
+        return bwd_stats_finish(part, (int)p.chunks, c, m, use_bn, mean, rstd, dgamma, dbeta, coef_out, scratch, cnt,
+                                st);
     int rc = reduce_slabs(part, (int)p.chunks, (int64_t)2 * c, sums, (int64_t)2 * c, (int64_t)2 * c, st);
     if (rc) return rc;
     if (coef_out) {  // statistics-only entry (unet_bn_relu_bwd_stats): no dz pass
@@ -555,9 +602,7 @@ extern "C" int unet_bn_relu_bwd(const float* da, const float* z, int64_t m, int 
 
 extern "C" size_t unet_bn_stats_partials_size(int S, int c) {
     if (S <= 0 || c <= 0) return 0;
-    size_t b = align_up((size_t)S * 2 * c * sizeof(float), 256);
-    if (S > kFinChunk) b += (size_t)cdiv(S, kFinChunk) * 2 * c * sizeof(double);
-    return b;
+    return bnpart_bytes(S, c);  // slabs | double scratch | in-launch finish counters (lastblock.h)
 }
 
 extern "C" int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, int c, const float* mean,
@@ -566,20 +611,10 @@ extern "C" int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, 
     UNET_CHECK_ARG(partials && coef && S > 0 && m > 0 && c > 0, "unet_bn_relu_bwd_stats_finish: bad args");
     UNET_CHECK_ARG(c % 4 == 0, "unet_bn_relu_bwd_stats_finish: channels must be a multiple of 4");
     UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_relu_bwd_stats_finish: use_bn needs mean/rstd");
-    hipStream_t st = as_stream(stream);
-    const unsigned gx = (unsigned)cdiv(c / 4, 16);
-    if (S <= kFinChunk) {
-        bn_bwd_finish_kernel<float><<<gx, 512, 0, st>>>(partials, S, c, m, use_bn, mean, rstd, dgamma, dbeta, coef);
-    } else {  // two passes: 256-slab chunk sums (double, in the buffer's tail), then the finish
-        const int nch = (int)cdiv(S, kFinChunk);
-        double* chunks = reinterpret_cast<double*>(reinterpret_cast<char*>(partials) +
-                                                   align_up((size_t)S * 2 * c * sizeof(float), 256));
-        bn_bwd_chunk_kernel<<<dim3(gx, (unsigned)nch), 512, 0, st>>>(partials, S, c, chunks);
-        UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats_finish(chunks)");
-        bn_bwd_finish_kernel<double><<<gx, 512, 0, st>>>(chunks, nch, c, m, use_bn, mean, rstd, dgamma, dbeta, coef);
-    }
-    UNET_CHECK_LAUNCH("unet_bn_relu_bwd_stats_finish");
-    return 0;
+    double* scratch = reinterpret_cast<double*>(reinterpret_cast<char*>(partials) + bnpart_scratch_off(S, c));
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(partials) + bnpart_counter_off(S, c));
+    return bwd_stats_finish(partials, S, c, m, use_bn, mean, rstd, dgamma, dbeta, coef, scratch, cnt,
+                            as_stream(stream));
 }
 
 extern "C" int unet_bn_relu_bwd_stats(const float* da, const float* z, int64_t m, int c, const float* mean,

@@ -477,7 +477,7 @@ class UNetEngine:
             if Sc > 0:
                 need = ops.bn_stats_partials_numel(K * Sc, view_in.channels)
                 if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
             for c in range(K):
                 sl = slice(c * nc, (c + 1) * nc)
                 if c > 0:  # chunk 0's data gradient was issued before the side-stream fork
@@ -505,7 +505,7 @@ class UNetEngine:
             if tb is not None:
                 need = ops.bn_stats_partials_numel(S, view_in.channels)
                 if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
                 ops.dwconv3x3_bwd(view_in, n, h, w, dk, dy, dx0, dx1, gdk, tb.mean if self.use_bn else None,
                                   tb.rstd if self.use_bn else None, tb.bnpart)
                 tb.bn_slabs = S
@@ -519,7 +519,7 @@ class UNetEngine:
                 tb = stats_target
                 need = ops.bn_stats_partials_numel(S, view_in.channels)
                 if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
                 ops.dwconv3x3_bwd_data_bnstats(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
                                                tb.rstd if self.use_bn else None, tb.bnpart)
                 tb.bn_slabs = S
@@ -561,7 +561,7 @@ class UNetEngine:
         if S > 0:  # the head's dx is all of the last block's da: emit its BN-backward partials too
             need = ops.bn_stats_partials_numel(S, hv.channels)
             if lb.bnpart is None or lb.bnpart.numel() < need:
-                lb.bnpart = torch.empty(need, dtype=torch.float32, device=self.device)
+                lb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
             ops.head_bwd_bnstats(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"], A.prob,
                                  y_true, A.sums, SMOOTH, loss_kind, lb.da, self.gvars["output_mask/kernel"],
                                  self.gvars["output_mask/bias"], lb.mean if self.use_bn else None,

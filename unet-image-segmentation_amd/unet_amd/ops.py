@@ -372,7 +372,10 @@ def bn_relu_bwd_stats(da: Tensor, z: Tensor, m: int, c: int, mean, rstd, scale, 
 
 
 def bn_stats_partials_numel(S: int, c: int) -> int:
-    """Floats of a producer-side BN partials buffer of S slabs (slabs + finish scratch)."""
+    """Floats of a producer-side BN partials buffer of S slabs (slabs + finish scratch + counters).
+
+    Allocate it zeroed (torch.zeros): bn_relu_bwd_stats_finish needs its counters zero on entry.
+    """
     return L.query("unet_bn_stats_partials_size", S, c) // 4
 
 
