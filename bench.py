@@ -93,7 +93,7 @@ def encoder_block_roofline(batch, size, device, reps=10):
             m = batch * hh * hh
             ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
-            part = torch.empty(ops.bn_partials_numel(m, co), device=device)
+            part = torch.zeros(ops.bn_partials_numel(m, co), device=device)
             fused = ops.sepconv_supported(view, batch, hh, hh, co)
 
             def run():

@@ -171,8 +171,12 @@ int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_ke
  * scale = gamma*rstd, shift = beta - mean*scale consumed by views; updates
  * moving stats when update_moving != 0.  gamma == NULL means
  * use_batch_norm=False: scale = 1, shift = beta (the sepconv bias).
- * The tail of bn_partials (past the per-tile partials) is scratch for the
- * two-pass reduction: the buffer must hold unet_bn_partials_size bytes.     */
+ * One launch: 64-partial chunk sums, then the last block of each 64-channel
+ * column to finish sums the chunk rows.  The tail of bn_partials (past the
+ * per-tile partials) holds the chunk rows and ceil(c/64) arrival counters:
+ * the buffer must hold unet_bn_partials_size bytes and its counters must be
+ * zero before the first call (allocate it zeroed once; calls leave them
+ * zero; the statistics producers never write past the per-tile partials).   */
 int unet_bn_finalize(float* bn_partials, int64_t m, int c,
                      const float* gamma, const float* beta, float eps,
                      float momentum, float* moving_mean, float* moving_var,

@@ -39,8 +39,9 @@ def test_view_struct_layout_matches_c():
 def test_workspace_queries():
     from unet_amd import _lib
     q = _lib.query
-    # ceil(1000/128) tiles x C x float2 (256-B aligned) + one chunk record x C x double2 of finalize scratch
-    assert q("unet_bn_partials_size", 1000, 64) == 8 * 64 * 8 + 1 * 64 * 16
+    # ceil(1000/128) tiles x C x float2 (256-B aligned) + one chunk record x C x double2 of finalize
+    # scratch (256-B aligned) + ceil(C/64) arrival counters
+    assert q("unet_bn_partials_size", 1000, 64) == 8 * 64 * 8 + 1 * 64 * 16 + 4
     assert q("unet_bn_partials_size", 0, 64) == 0
     # BN-backward slabs [S][2C] float | double chunk rows, one per 64 slabs | ceil(C/64) counters
     assert q("unet_bn_stats_partials_size", 300, 64) == 300 * 128 * 4 + 5 * 128 * 8 + 1 * 4

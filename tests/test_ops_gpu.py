@@ -128,7 +128,7 @@ def test_pointwise_and_bn_stats(ops, m, cin, cout, off):
     y = f32(rng.standard_normal((m, cin)) + off)
     pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cin))
     z = torch.empty((m, cout), device="cuda")
-    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
     ops.pointwise_fwd(dev(y), m, cin, cout, dev(pk), z, part)
     zr = y @ pk[0, 0]
     assert rel_err(host(z), zr) < 5e-6
@@ -147,6 +147,11 @@ def test_pointwise_and_bn_stats(ops, m, cin, cout, off):
     assert rel_err(host(outs[2]), inv) < 1e-5
     assert rel_err(host(outs[3]), beta - mean * inv) < 1e-4
     assert rel_err(host(tm), mm2) < 1e-5 and rel_err(host(tv), mv2) < 1e-5
+    # again: the finalize's arrival counters were left zero, the result is bitwise the same
+    outs2 = [torch.empty(cout, device="cuda") for _ in range(4)]
+    ops.bn_finalize(part, m, cout, dev(gamma), dev(beta), 1e-3, 0.99, None, None, False, *outs2)
+    assert all(torch.equal(a, b) for a, b in zip(outs, outs2))
+    assert not torch.any(part[-((cout + 63) // 64):].view(torch.int32))
     # no-partials path (inference GEMM epilogue)
     z2 = torch.empty((m, cout), device="cuda")
     ops.pointwise_fwd(dev(y), m, cin, cout, dev(pk), z2, None)
@@ -378,7 +383,7 @@ def test_fused_sepconv(ops, mode, n, h, w, c0, c1, cout, drop, train):
     m = n * h * w
     y = torch.full((n, h, w, C), -7.0, device="cuda")
     z = torch.empty((n, h, w, cout), device="cuda")
-    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
     ops.sepconv_fwd(v, n, h, w, dev(dk), cout, dev(pk), y if train else None, z, part if train else None)
     xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 77)
     yr = K.depthwise3x3(xv, dk)

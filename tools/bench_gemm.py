@@ -28,7 +28,7 @@ res = []
 for hw, cin, cout in blocks:
     m = B * hw * hw
     y, pk, z = t(m, cin), t(cin, cout) * 0.1, t(m, cout)
-    part = torch.empty(ops.bn_partials_numel(m, cout), device=dev)
+    part = torch.zeros(ops.bn_partials_numel(m, cout), device=dev)
     dz, dy, dpk = t(m, cout), t(m, cin), t(cin, cout)
     fl = 2.0 * m * cin * cout
     r = {"hw": hw, "cin": cin, "cout": cout}

@@ -59,7 +59,7 @@ for mode, h, w, c0, c1, cout in SHAPES:
     dz = torch.randn(N, h, w, cout, device="cuda")
     dz2 = torch.empty(N, h, w, cout, device="cuda")
     dy = torch.randn(N, h, w, C, device="cuda")
-    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
     ddk = torch.empty(3, 3, C, 1, device="cuda")
     dpk = torch.empty(1, 1, C, cout, device="cuda")
     gf = 2.0 * m * C * cout

@@ -44,7 +44,7 @@ for mode, h, w, c0, c1, cout in SHAPES:
     pk = torch.randn(1, 1, C, cout, device="cuda") * 0.05
     y = torch.empty(N, h, w, C, device="cuda")
     z = torch.empty(N, h, w, cout, device="cuda")
-    part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+    part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
     fused = timeit(lambda: ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part))
     infer = timeit(lambda: ops.sepconv_fwd(v, N, h, w, dk, cout, pk, None, z, None))
 

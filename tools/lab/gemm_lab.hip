@@ -45,6 +45,9 @@ int main(int argc, char** argv) {
         {16384, 1024, 512, 0}, {16384, 4096, 512, 0}, {65536, 2048, 256, 0}, {8192, 4096, 512, 0}, {32768, 4096, 512, 0},
         {1048576, 64, 64, 1}, {1048576, 64, 128, 1}, {262144, 128, 128, 1}, {262144, 128, 256, 1}, {65536, 256, 256, 1},
         {16384, 512, 512, 1}, {16384, 512, 1024, 1}, {4096, 1024, 1024, 1},
+        // Conv2DTranspose fwd (mode 2: N = 4 cout) and data gradient (mode 3: K = 4 cout), batch 16
+        {262144, 128, 256, 2}, {65536, 256, 512, 2}, {16384, 512, 1024, 2}, {4096, 1024, 2048, 2},
+        {262144, 256, 128, 3}, {65536, 512, 256, 3}, {16384, 1024, 512, 3}, {4096, 2048, 1024, 3},
     };
     const char* only = getenv("LAB_SHAPE");
     int si = -1;
@@ -52,6 +55,7 @@ int main(int argc, char** argv) {
         ++si;
         if (only && atoi(only) != si) continue;
         const int64_t M = s.M; const int K = s.K, N = s.N;
+        if (getenv("LAB_MODE") && atoi(getenv("LAB_MODE")) != s.mode) continue;
         float* A = dalloc(M * K, 1.f, 1);
         float* Z = dalloc(M * K, 1.f, 2);
         float* B = dalloc((size_t)K * N, 0.1f, 3);
@@ -59,16 +63,21 @@ int main(int argc, char** argv) {
         float* C1; CK(hipMalloc(&C1, M * N * 4));
         float* side; CK(hipMalloc(&side, M * K * 4));
         float2* stats; CK(hipMalloc(&stats, (M / 32 + 1) * N * 8));
-        float* sc = dalloc(K, 1.f, 4); float* sh = dalloc(K, 0.5f, 5); float* coef = dalloc(3 * K, 0.1f, 6);
+        float* sc = dalloc(K > N ? K : N, 1.f, 4); float* sh = dalloc(K, 0.5f, 5); float* coef = dalloc(3 * K, 0.1f, 6);
         RowsArgs a{};
         unet_view v{}; v.mode = UNET_VIEW_PLAIN; v.c0 = K; v.src0 = A;
         a.a = make_dview(v);
         a.M = M; a.K = K; a.N = N; a.B = B; a.ldc = N;
+        const int hw = (int)lround(sqrt((double)(M / 16)));  // convT shapes: batch 16, square levels
         if (s.mode == 0) { a.sbk = N; a.sbn = 1; a.stats = stats; }
+        else if (s.mode == 2) { a.sbk = 1; a.sbn = K; a.bias = sc; a.sH = hw; a.sW = hw; a.sf = N / 4; }
+        else if (s.mode == 3) {  // A = dU (n, 2h, 2w, K/4) read unshuffled: M x K elements either way
+            a.a.c0 = K / 4; a.uH = hw; a.uW = hw; a.uf = K / 4; a.sbk = N; a.sbn = 1; a.ldc = N; }
         else { a.sbk = 1; a.sbn = K; a.a.sc0 = sc; a.a.sh0 = sh; a.a.rate = 0.2f; a.a.inv_keep = 1.25f; a.a.seed = 77;
                a.z = Z; a.coef = coef; a.side = side; }
         const double fl = 2.0 * M * K * N;
-        printf("M=%ld K=%d N=%d %s\n", (long)M, K, N, s.mode == 0 ? "fwd+stats" : "dgrad_bnbwd+drop");
+        static const char* mname[4] = {"fwd+stats", "dgrad_bnbwd+drop", "convT fwd", "convT dgrad"};
+        printf("M=%ld K=%d N=%d %s\n", (long)M, K, N, mname[s.mode]);
         run_variants(s.mode, a, C0, C1, fl, M * N);
         CK(hipFree(A)); CK(hipFree(Z)); CK(hipFree(B)); CK(hipFree(C0)); CK(hipFree(C1)); CK(hipFree(side));
         CK(hipFree(stats)); CK(hipFree(sc)); CK(hipFree(sh)); CK(hipFree(coef));

@@ -18,7 +18,7 @@ dk = torch.randn(3, 3, C, 1, device="cuda")
 pk = torch.randn(1, 1, C, cout, device="cuda") * 0.05
 y = torch.empty(N, h, w, C, device="cuda")
 z = torch.empty(N, h, w, cout, device="cuda")
-part = torch.empty(ops.bn_partials_numel(m, cout), device="cuda")
+part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
 for _ in range(iters):
     if split:
         ops.dwconv3x3_fwd(v, N, h, w, dk, y)

@@ -20,13 +20,12 @@ constexpr int kStatsRows = 128;
 // S2 = sum M2_b + n_b (mean_b - K)^2, in double, fixed order (4 lanes, then lane order).
 // Coalesced: consecutive threads read consecutive channels of one partial row.
 constexpr int kChunkParts = 64;
-__global__ __launch_bounds__(256) void bn_stats_chunk_kernel(const float2* __restrict__ part, int64_t nblk, int64_t M,
-                                                             int C, double2* __restrict__ chunks) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int lane = threadIdx.x >> 6;
-    const int64_t b0 = (int64_t)blockIdx.y * kChunkParts;
+__device__ __forceinline__ void chunk_sums(const float2* __restrict__ part, int64_t nblk, int64_t M, int C, int c,
+                                           int lane, int chunk, double& s1, double& s2) {
+    const int64_t b0 = (int64_t)chunk * kChunkParts;
     const int64_t b1 = b0 + kChunkParts < nblk ? b0 + kChunkParts : nblk;
-    double s1 = 0.0, s2 = 0.0;
+    s1 = 0.0;
+    s2 = 0.0;
     if (c < C) {
         const double K = (double)part[c].x;
 #pragma unroll 4
@@ -39,48 +38,18 @@ __global__ __launch_bounds__(256) void bn_stats_chunk_kernel(const float2* __res
             s2 += (double)pm.y + nd * d;
         }
     }
-    __shared__ double r1[256], r2[256];
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = s2;
-    __syncthreads();
-    if (lane == 0 && c < C) {
-        for (int l = 1; l < 4; ++l) {
-            s1 += r1[threadIdx.x + 64 * l];
-            s2 += r2[threadIdx.x + 64 * l];
-        }
-        chunks[(int64_t)blockIdx.y * C + c] = make_double2(s1, s2);
-    }
 }
 
-// Pass 2: per channel, chunk sums (4 lanes over interleaved chunks, combined in lane order)
-// -> mean, biased var, folded affine, moving update.  64 channels per block.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const double2* __restrict__ chunks, int nch,
-                                                          const float2* __restrict__ part, int64_t M, int C,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps, float momentum,
-                                                          float* moving_mean, float* moving_var, int update_moving,
-                                                          float* mean_out, float* rstd_out, float* scale_out,
-                                                          float* shift_out) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int lane = threadIdx.x >> 6;
-    double s1 = 0.0, s2 = 0.0;
-    if (c < C) {
-#pragma unroll 8
-        for (int k = lane; k < nch; k += 4) {
-            const double2 v = chunks[(int64_t)k * C + c];
-            s1 += v.x;
-            s2 += v.y;
-        }
-    }
-    __shared__ double r1[256], r2[256];
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = s2;
-    __syncthreads();
-    if (lane != 0 || c >= C) return;
-    for (int l = 1; l < 4; ++l) {
-        s1 += r1[threadIdx.x + 64 * l];
-        s2 += r2[threadIdx.x + 64 * l];
-    }
+// Pass 2 (same launch, lastblock.h): every block publishes its chunk row (sc1 stores); the last
+// block of each 64-channel column to arrive sums the rows (4 lanes over interleaved chunks,
+// combined in lane order) -> mean, biased var, folded affine, moving update.  One chunk: the
+// block's own sums are final.
+__device__ __forceinline__ void bn_finalize_channel(int c, double s1, double s2, const float2* __restrict__ part,
+                                                    int64_t M, const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, float eps, float momentum,
+                                                    float* moving_mean, float* moving_var, int update_moving,
+                                                    float* mean_out, float* rstd_out, float* scale_out,
+                                                    float* shift_out) {
     const double dm = s1 / (double)M;
     const float mean = (float)((double)part[c].x + dm);
     double vd = s2 / (double)M - dm * dm;
@@ -100,6 +69,58 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double2* __restr
         moving_mean[c] = moving_mean[c] * momentum + mean * (1.0f - momentum);
         moving_var[c] = moving_var[c] * momentum + var * (1.0f - momentum);
     }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restrict__ part, int64_t nblk, int64_t M,
+                                                          int C, double* __restrict__ chunks, unsigned* cnt,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float momentum,
+                                                          float* moving_mean, float* moving_var, int update_moving,
+                                                          float* mean_out, float* rstd_out, float* scale_out,
+                                                          float* shift_out) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int lane = threadIdx.x >> 6;
+    const int nch = gridDim.y;
+    double s1, s2;
+    chunk_sums(part, nblk, M, C, c, lane, blockIdx.y, s1, s2);
+    __shared__ double r1[256], r2[256];
+    __shared__ int flag;
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    if (lane == 0 && c < C)
+        for (int l = 1; l < 4; ++l) {
+            s1 += r1[threadIdx.x + 64 * l];
+            s2 += r2[threadIdx.x + 64 * l];
+        }
+    if (nch > 1) {
+        if (lane == 0 && c < C) {
+            st_agent(chunks + ((int64_t)blockIdx.y * C + c) * 2, s1);
+            st_agent(chunks + ((int64_t)blockIdx.y * C + c) * 2 + 1, s2);
+        }
+        if (!last_arrival(cnt + blockIdx.x, (unsigned)nch, &flag)) return;
+        s1 = 0.0;
+        s2 = 0.0;
+        if (c < C) {
+#pragma unroll 8
+            for (int k = lane; k < nch; k += 4) {
+                s1 += ld_agent(chunks + ((int64_t)k * C + c) * 2);
+                s2 += ld_agent(chunks + ((int64_t)k * C + c) * 2 + 1);
+            }
+        }
+        __syncthreads();  // r1/r2 were read above by lane 0 before the arrival barrier; reuse
+        r1[threadIdx.x] = s1;
+        r2[threadIdx.x] = s2;
+        __syncthreads();
+        if (lane == 0 && c < C)
+            for (int l = 1; l < 4; ++l) {
+                s1 += r1[threadIdx.x + 64 * l];
+                s2 += r2[threadIdx.x + 64 * l];
+            }
+    }
+    if (lane != 0 || c >= C) return;
+    bn_finalize_channel(c, s1, s2, part, M, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving,
+                        mean_out, rstd_out, scale_out, shift_out);
 }
 
 __global__ void bn_infer_kernel(const float* gamma, const float* beta, const float* mm, const float* mv, int C,
@@ -478,8 +499,9 @@ using namespace unet;
 
 size_t unet::bn_partials_bytes(int64_t m, int c) {
     const int64_t nblk = cdiv(m, kStatsRows);
-    return align_up((size_t)nblk * c * sizeof(float2), 256) +
-           (size_t)cdiv(nblk, kChunkParts) * c * sizeof(double2);
+    return align_up((size_t)nblk * c * sizeof(float2), 256) +  // per-tile partials
+           align_up((size_t)cdiv(nblk, kChunkParts) * c * sizeof(double2), 256) +  // chunk rows
+           (size_t)cdiv(c, 64) * sizeof(unsigned);  // finalize arrival counters (zero at allocation)
 }
 
 extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const float* gamma, const float* beta,
@@ -491,13 +513,14 @@ extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const floa
     const int64_t nblk = cdiv(m, kStatsRows);
     const int nch = (int)cdiv(nblk, kChunkParts);
     const float2* part = reinterpret_cast<const float2*>(bn_partials);
-    double2* chunks = reinterpret_cast<double2*>(reinterpret_cast<char*>(bn_partials) +
-                                                 align_up((size_t)nblk * c * sizeof(float2), 256));
-    bn_stats_chunk_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, st>>>(part, nblk, m, c, chunks);
-    UNET_CHECK_LAUNCH("unet_bn_finalize(chunks)");
-    bn_finalize_kernel<<<(unsigned)cdiv(c, 64), 256, 0, st>>>(chunks, nch, part, m, c, gamma, beta, eps, momentum,
-                                                               moving_mean, moving_var, update_moving, mean, rstd,
-                                                               scale, shift);
+    double* chunks = reinterpret_cast<double*>(reinterpret_cast<char*>(bn_partials) +
+                                               align_up((size_t)nblk * c * sizeof(float2), 256));
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(bn_partials) +
+                                                align_up((size_t)nblk * c * sizeof(float2), 256) +
+                                                align_up((size_t)nch * c * sizeof(double2), 256));
+    bn_finalize_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, st>>>(
+        part, nblk, m, c, chunks, cnt, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving, mean, rstd,
+        scale, shift);
     UNET_CHECK_LAUNCH("unet_bn_finalize");
     return 0;
 }

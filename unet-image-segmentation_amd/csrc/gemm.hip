@@ -17,6 +17,7 @@
 // images, so each MFMA operand fetch is one conflict-free ds_read_b32 per lane), double
 // buffered: the next stage's global loads are in flight while the current stage's MFMAs run.
 // The A operand passes through an activation view (BN+ReLU / dropout / unshuffle) on load.
+#include <cstdlib>
 #include "view.h"
 
 namespace unet {
@@ -946,7 +947,13 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     w.bp = P > 64 ? 128 : 64;
     w.bq = Q > 64 ? 128 : 64;
     w.tiles = (int)(cdiv(P, w.bp) * cdiv(Q, w.bq));
-    int64_t want = cdiv(1024, w.tiles);  // ~4 blocks per CU
+    static int target = -1;  // ~4 blocks per CU (UNET_WGRAD_BLOCKS: tuning; read once per process)
+    if (target < 0) {
+        const char* e = getenv("UNET_WGRAD_BLOCKS");
+        target = e ? atoi(e) : 1024;
+        if (target < 1) target = 1024;
+    }
+    int64_t want = cdiv(target, w.tiles);
     int64_t maxs = M / 512;               // >= 32 k-steps per block: fewer, cheaper slabs
     if (maxs < 1) maxs = 1;
     int64_t S = want < maxs ? want : maxs;

@@ -164,7 +164,7 @@ class UNetEngine:
         # contending with the HBM-bound 256x256 / 128x128 data-gradient chain (measured 1272 ->
         # 1296 img/s, r1za).  With all-reduce hooks the low-water mark is held back until the
         # deferred work is issued, so buckets still complete from the end of the flat buffer.
-        dl = os.environ.get("UNET_DEFER_WGRAD", "0,1")
+        dl = os.environ.get("UNET_DEFER_WGRAD", "")
         self.defer_wgrad_levels = {int(t) for t in dl.split(",") if t.strip()}
         # Conv2DTranspose weight / bias gradients on the side stream (its data gradient stays on
         # the critical path); the side stream is otherwise idle until the deferred work is issued
@@ -236,7 +236,7 @@ class UNetEngine:
             max_out = max(max_out, m * b.cout)
             blocks[b.name] = BlockBufs(
                 y=torch.empty((n, h, w, b.cin), **f32), z=torch.empty((n, h, w, b.cout), **f32),
-                part=torch.empty(ops.bn_partials_numel(m, b.cout), **f32),
+                part=torch.zeros(ops.bn_partials_numel(m, b.cout), **f32),
                 mean=torch.zeros(b.cout, **f32), rstd=torch.zeros(b.cout, **f32),
                 scale=torch.zeros(b.cout, **f32), shift=torch.zeros(b.cout, **f32),
                 da=torch.empty((n, h, w, b.cout), **f32))

@@ -45,7 +45,7 @@ class ConvBlock:
         ops.dwconv3x3_fwd(View.plain(x.contiguous()), n, h, w, self.vars["depthwise_kernel"], y)
         v = self.vars
         if self.use_bn and training:
-            part = torch.empty(ops.bn_partials_numel(m, self.cout), dtype=torch.float32, device=x.device)
+            part = torch.zeros(ops.bn_partials_numel(m, self.cout), dtype=torch.float32, device=x.device)
             ops.pointwise_fwd(y, m, c, self.cout, v["pointwise_kernel"], z, part)
             ops.bn_finalize(part, m, self.cout, v["gamma"], v["beta"], BN_EPS, BN_MOMENTUM, v["moving_mean"],
                             v["moving_variance"], True, self.mean, self.rstd, self.scale, self.shift)

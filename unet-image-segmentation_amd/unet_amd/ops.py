@@ -268,6 +268,7 @@ def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
 
 
 def bn_partials_numel(m: int, c: int) -> int:
+    """Floats of a forward BN partials buffer; allocate it zeroed (bn_finalize's counters)."""
     return L.query("unet_bn_partials_size", m, c) // 4
 
 
