@@ -278,6 +278,22 @@ def test_conv_transpose(ops, mode, drop, n, h, w, cin, cout):
     assert rel_err(host(db), rdb) < 5e-6
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("cin", [32, 64, 128, 256, 48])  # 48: the LDS-tile kernel
+@pytest.mark.parametrize("n,h,w", [(2, 12, 10), (1, 3, 5), (3, 64, 40)])  # ragged pixel counts; > 1 grid pass
+def test_head_fwd_binary(ops, mode, cin, n, h, w):
+    """Binary sigmoid head (u_net.py:105-112) against the float64 oracle."""
+    rng = np.random.default_rng(cin + 3 * mode + n * h * w)
+    a, t = _view_inputs(rng, mode, n, h, w, cin)
+    v = _mk_view(ops, mode, t)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"))
+    k = f32(rng.standard_normal((1, 1, cin, 1)) * 0.2)
+    b = f32(rng.standard_normal(1) * 0.1)
+    prob = torch.full((n, h, w, 1), -1.0, device="cuda")
+    ops.head_fwd(v, n, h, w, 1, dev(k), dev(b), prob)
+    assert rel_err(host(prob), K.head(xv, k, b, 1)) < 2e-6
+
+
 @pytest.mark.parametrize("ncls", [1, 21])
 @pytest.mark.parametrize("loss_kind", [0, 1])
 def test_head_dice(ops, ncls, loss_kind):
@@ -406,6 +422,52 @@ def test_fused_sepconv_unsupported_shapes(ops):
     assert not ops.sepconv_supported(ops.View.plain(x), 1, 8, 8, 64)     # w % 16 != 0
     x3 = torch.zeros((1, 16, 16, 3), device="cuda")
     assert not ops.sepconv_supported(ops.View.plain(x3), 1, 16, 16, 64)  # 3 channels
+
+
+@pytest.mark.parametrize("use_bn", [True, False])
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 8, 8, 128, 64), (1, 5, 7, 64, 32), (3, 4, 6, 256, 128),
+                                            (2, 16, 16, 128, 128), (4, 64, 144, 128, 64)])  # > 256 slabs
+def test_convt_bwd_data_bnstats(ops, use_bn, n, h, w, cin, cout):
+    """Conv2DTranspose data gradient that also emits the BN-backward partials of the block below
+    (u_net.py:88 upsample fed by a BN+ReLU output): dx bitwise equal to the plain launch,
+    statistics equal to unet_bn_relu_bwd_stats's and to float64 numpy."""
+    rng = np.random.default_rng(n * 1000 + h * 10 + cin + cout)
+    a, t = _view_inputs(rng, 1, n, h, w, cin)
+    v = _mk_view(ops, 1, t)
+    k = dev(f32(rng.standard_normal((2, 2, cout, cin)) * 0.1))
+    dout = dev(f32(rng.standard_normal((n, 2 * h, 2 * w, cout))))
+    S = ops.conv_transpose2x2_bwd_data_bnstats_slabs(v, n, h, w, cout)
+    m = n * h * w
+    assert S == (m + 127) // 128
+    assert ops.conv_transpose2x2_bwd_data_bnstats_slabs(v.dropout(0.2, 1), n, h, w, cout) == 0
+    mean = dev(f32(rng.standard_normal(cin) * 0.1))
+    rstd = dev(f32(1.0 + rng.random(cin)))
+    part = torch.zeros(ops.bn_stats_partials_numel(S, cin), device="cuda")  # counters zero
+    dx_f, dx_p = torch.empty((n, h, w, cin), device="cuda"), torch.empty((n, h, w, cin), device="cuda")
+    ops.conv_transpose2x2_bwd_data_bnstats(v, n, h, w, cout, k, dout, dx_f, mean if use_bn else None,
+                                           rstd if use_bn else None, part)
+    ops.conv_transpose2x2_bwd(v, n, h, w, cout, k, dout, dx_p, None, None)
+    assert torch.equal(dx_f, dx_p)
+    outs = []
+    for fused in (True, False):
+        dg, db, coef = (torch.zeros(cin, device="cuda"), torch.zeros(cin, device="cuda"),
+                        torch.empty(3 * cin, device="cuda"))
+        if fused:
+            ops.bn_relu_bwd_stats_finish(part, S, m, cin, mean, rstd, use_bn, dg if use_bn else None, db, coef)
+            assert not torch.any(part[-((cin + 63) // 64):].view(torch.int32))
+        else:
+            ops.bn_relu_bwd_stats(dx_p, t["src0"], m, cin, mean, rstd, t["sc0"], t["sh0"], use_bn, 0.0, 0,
+                                  dg if use_bn else None, db, coef)
+        outs.append((host(dg), host(db), host(coef)))
+    for x, y in zip(outs[0], outs[1]):
+        assert rel_err(x, y) < 2e-5
+    da = host(dx_p).astype(np.float64).reshape(-1, cin)
+    z = a["src0"].astype(np.float64).reshape(-1, cin)
+    g = np.where(z * a["sc0"] + a["sh0"] > 0, da, 0.0)
+    assert rel_err(outs[0][1], g.sum(0)) < 1e-5
+    if use_bn:
+        xh = (z - host(mean)) * host(rstd)
+        assert rel_err(outs[0][0], (g * xh).sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("mode", [2, 1])

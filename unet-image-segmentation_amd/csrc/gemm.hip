@@ -35,7 +35,11 @@ constexpr int kStatsRows = 128;  // rows per BatchNorm partial (= BM of the stat
 // gradient da (a.src0) and the raw pre-BN z: g = da * drop * [z*sc+sh > 0],
 // dz = sc * (g - p - (z - mu) * q) with per-channel (mu, p, q) = coef[0..3C) (see bn.hip).
 enum { A_PLAIN = 0, A_BNRELU = 1, A_UNSHUFFLE = 2, A_BNBWD = 3 };
-enum { E_STORE = 0, E_STATS = 1, E_SHUFFLE = 2 };
+// E_BNPART: E_STORE, and the stored C is the complete da of a BatchNorm + ReLU block whose raw
+// z is g.z (same [M][N] layout): the tile also emits that block's BN-backward partial sums
+// bnpart[tile][0][n] = sum g, bnpart[tile][1][n] = sum g * xhat, g = da * [z*sc+sh > 0],
+// xhat = (z - mu) * rs (the dwtile.hip STATS format, finished by unet_bn_relu_bwd_stats_finish).
+enum { E_STORE = 0, E_STATS = 1, E_SHUFFLE = 2, E_BNPART = 3 };
 
 struct RowsArgs {
     DView a;  // A operand: PLAIN/BNRELU -> a.src0[m * a.c0 + k]; UNSHUFFLE -> a.src0 = dU
@@ -53,6 +57,8 @@ struct RowsArgs {
     const float* z;     // A_BNBWD: pre-BN z (same layout as a.src0)
     const float* coef;  // A_BNBWD: (mu, p, q) x C
     float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
+    const float *bsc, *bsh, *bmu, *brs;  // E_BNPART: per-column BN scale/shift, mean/rstd (NULL: no xhat)
+    float* bnpart;                       // E_BNPART: [cdiv(M, 128)][2][N] partial sums
 };
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
@@ -610,7 +616,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     }
 
     const bool full = M_rem == BM;  // every row of the tile exists: no per-row checks
-    if constexpr (EPI == E_STORE || EPI == E_STATS) {
+    if constexpr (EPI == E_STORE || EPI == E_STATS || EPI == E_BNPART) {
         const int ldc = (int)g.ldc;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
@@ -676,6 +682,55 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                     o.y = a.y + b.y + d * d * na * f;
                 }
                 if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = o;
+            }
+        }
+    }
+    if constexpr (EPI == E_BNPART) {
+        // per column: this lane's 16*TM rows, the other row half (hi), then the other wave row (LDS);
+        // fixed order, so the partials are deterministic
+        float2* red = reinterpret_cast<float2*>(&As[0][0]);
+        const int ldc = (int)g.ldc;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * (BN / 2) + tn * 32 + lo;
+            const int n = n0 + col;
+            float s1 = 0.f, s2 = 0.f;
+            if (n < g.N) {
+                const float sc = g.bsc[n], sh = g.bsh[n];
+                const float mu = g.bmu ? g.bmu[n] : 0.f, rs = g.brs ? g.brs[n] : 0.f;
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const int rb0 = wm * (BM / 2) + tm * 32 + 4 * hi;
+                    const float* zp = g.z + (int64_t)(m0 + rb0) * g.ldc + n;
+                    float zv[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        zv[r] = (full || rb0 + acc_row(r, 0) < M_rem) ? zp[acc_row(r, 0) * ldc] : 0.f;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const bool in = full || rb0 + acc_row(r, 0) < M_rem;
+                        const float gm = (in && fmaf(zv[r], sc, sh) > 0.f) ? acc[tm][tn][r] : 0.f;
+                        s1 += gm;
+                        s2 = fmaf(gm, (zv[r] - mu) * rs, s2);
+                    }
+                }
+            }
+            s1 += __shfl_xor(s1, 32, 64);
+            s2 += __shfl_xor(s2, 32, 64);
+            if (hi == 0) red[wm * BN + col] = make_float2(s1, s2);
+        }
+        __syncthreads();
+        if (wm == 0 && hi == 0) {
+            float* out = g.bnpart + (int64_t)blockIdx.x * 2 * g.N;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * (BN / 2) + tn * 32 + lo;
+                const int n = n0 + col;
+                const float2 a = red[col], b = red[BN + col];
+                if (n < g.N) {
+                    out[n] = a.x + b.x;
+                    out[g.N + n] = a.y + b.y;
+                }
             }
         }
     }
@@ -922,7 +977,7 @@ int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
         UNET_CHECK_LAUNCH(what);
         return 0;
     }
-    if constexpr (AMODE == A_BNBWD) {  // vectorised kernel only
+    if constexpr (AMODE == A_BNBWD || EPI == E_BNPART) {  // vectorised kernel only
         UNET_CHECK_ARG(false, "%s: needs channel counts divisible by 4 and 16-B aligned operands", what);
     } else {
         const unsigned gm = (unsigned)cdiv(a.M, 128);
@@ -1253,6 +1308,51 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
                        "unet_conv_transpose2x2_bwd(filter)");
     if (rc) return rc;
     return colsum(dout, 4 * M, cout, dbias, ws, ws_bytes, st);
+}
+
+extern "C" int unet_conv_transpose2x2_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w, int cout) {
+    if (!x || x->mode != UNET_VIEW_BNRELU || x->drop_rate != 0.f || n <= 0 || h <= 0 || w <= 0 || cout <= 0)
+        return 0;
+    if (x->c0 % 4 || cout % 4) return 0;
+    const int64_t M = (int64_t)n * h * w;
+    if (!fits_i32(M, x->c0) || !fits_i32(4 * M, cout)) return 0;
+    return (int)cdiv(M, 128);
+}
+
+extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h, int w, int cout,
+                                                       const float* kernel, const float* dout, float* dx,
+                                                       const float* mean, const float* rstd, float* bn_partials,
+                                                       unet_stream_t stream) {
+    if (check_view(x, "unet_conv_transpose2x2_bwd_data_bnstats")) return -1;
+    const int S = unet_conv_transpose2x2_bwd_data_bnstats_slabs(x, n, h, w, cout);
+    UNET_CHECK_ARG(S > 0, "unet_conv_transpose2x2_bwd_data_bnstats: needs a BNRELU view without dropout and "
+                          "channel counts divisible by 4");
+    UNET_CHECK_ARG(kernel && dout && dx && bn_partials && x->scale0 && x->shift0,
+                   "unet_conv_transpose2x2_bwd_data_bnstats: bad args");
+    UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_conv_transpose2x2_bwd_data_bnstats: mean/rstd go together");
+    const int cin = x->c0;
+    RowsArgs a{};
+    a.a = plain_view(dout, cout);
+    a.M = (int64_t)n * h * w;
+    a.K = 4 * cout;
+    a.uH = h;
+    a.uW = w;
+    a.uf = cout;
+    a.B = kernel;
+    a.sbk = cin;
+    a.sbn = 1;
+    a.N = cin;
+    a.C = dx;
+    a.ldc = cin;
+    a.z = x->src0;
+    a.bsc = x->scale0;
+    a.bsh = x->shift0;
+    a.bmu = mean;
+    a.brs = rstd;
+    a.bnpart = bn_partials;
+    UNET_CHECK_ARG(rows_vec_ok(a, A_UNSHUFFLE) && ((uintptr_t)dx | (uintptr_t)x->src0) % 16 == 0,
+                   "unet_conv_transpose2x2_bwd_data_bnstats: operands must be 16-B aligned");
+    return launch_rows<A_UNSHUFFLE, false, E_BNPART>(a, as_stream(stream), "unet_conv_transpose2x2_bwd_data_bnstats");
 }
 
 namespace unet {

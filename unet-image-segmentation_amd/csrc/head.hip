@@ -4,8 +4,9 @@
 //                                                                      utils/loss.py:9-48
 //   MeanIoU   : keras.metrics.MeanIoU(num_classes)                     scripts/train.py:231,
 //                                                                      scripts/benchmark.py:237-277
-// The head is HBM-bound (64 -> ncls per pixel): one lane per pixel, the (Cin x ncls)
-// kernel in LDS (broadcast reads).  Dice sums are per (image, class) over H*W: per-block
+// The head is HBM-bound (64 -> ncls per pixel).  Binary: a lane group per pixel, xor-shuffle
+// dot products (head_fwd_bin_kernel); multi-class: one lane per pixel, the (Cin x ncls) kernel in
+// LDS (broadcast reads).  Dice sums are per (image, class) over H*W: per-block
 // partials, then one fixed-order finalize in double.
 #include "view.h"
 
@@ -21,6 +22,55 @@ namespace {
 
 constexpr int kMaxCin = 256;
 constexpr int kMaxCls = 32;
+
+// Binary head, Cin = 4G (G lanes per pixel, one channel quad each): every lane issues U
+// independent float4 loads (U pixels, each wave's loads contiguous 1 KB runs), applies the
+// BN+ReLU view, dots with its kernel quad held in registers, and the G lanes of a pixel reduce
+// with xor shuffles.  No LDS, no barriers: the loads of a wave stay in flight together.
+template <int MODE, int G>
+__global__ __launch_bounds__(256) void head_fwd_bin_kernel(DView v, int64_t M, const float* __restrict__ W,
+                                                           const float* __restrict__ bias, float* __restrict__ prob) {
+    constexpr int PPW = 64 / G;  // pixels per wave per slot
+    constexpr int U = 4;
+    constexpr int PB = 4 * U * PPW;  // pixels per block iteration
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = lane % G, ps = lane / G;
+    const int c = 4 * q;
+    const float4 wk = ld4(W + c);  // Keras (1, 1, Cin, 1): W[c]
+    float4 sc = f4(1.f), sh = f4(0.f);
+    if constexpr (MODE == UNET_VIEW_BNRELU) {
+        sc = ld4(v.sc0 + c);
+        sh = ld4(v.sh0 + c);
+    }
+    const float b = bias ? bias[0] : 0.f;
+    for (int64_t base = (int64_t)blockIdx.x * PB; base < M; base += (int64_t)gridDim.x * PB) {
+        const int64_t p0 = base + wave * U * PPW + ps;
+        float4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t m = p0 + u * PPW;
+            x[u] = m < M ? ld4(v.src0 + m * (4 * G) + c) : f4(0.f);
+        }
+        float s[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float4 a = x[u];
+            if constexpr (MODE == UNET_VIEW_BNRELU) a = bnrelu4(a, sc, sh);
+            s[u] = fmaf(a.x, wk.x, fmaf(a.y, wk.y, fmaf(a.z, wk.z, a.w * wk.w)));
+        }
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1)
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off, 64);
+        if (q == 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = p0 + u * PPW;
+                if (m < M) prob[m] = 1.0f / (1.0f + expf(-(s[u] + b)));
+            }
+        }
+    }
+}
 
 // Pixel tile of TP = 8192 / Cin (binary) or 4096 / Cin (multi-class) pixels: the tile's activations are staged through LDS with
 // coalesced float4 loads (one lane per channel quad), then one lane per pixel forms the logits.
@@ -430,6 +480,28 @@ extern "C" int unet_head_fwd(const unet_view* x, int n, int h, int w, int ncls, 
     const DView v = make_dview(*x);
     const int64_t M = (int64_t)n * h * w;
     hipStream_t st = as_stream(stream);
+    const bool bin_vec = ncls == 1 && (x->c0 == 32 || x->c0 == 64 || x->c0 == 128 || x->c0 == 256) &&
+                         ((uintptr_t)x->src0 | (uintptr_t)kernel) % 16 == 0;
+    if (bin_vec) {
+        const int G = x->c0 / 4;
+        const int64_t gb = cdiv(M, (int64_t)16 * (64 / G));
+        const int grid = (int)(gb > 4096 ? 4096 : gb);
+#define UNET_HB(MODE_)                                                                                       \
+    switch (G) {                                                                                             \
+        case 8: head_fwd_bin_kernel<MODE_, 8><<<grid, 256, 0, st>>>(v, M, kernel, bias, prob); break;         \
+        case 16: head_fwd_bin_kernel<MODE_, 16><<<grid, 256, 0, st>>>(v, M, kernel, bias, prob); break;       \
+        case 32: head_fwd_bin_kernel<MODE_, 32><<<grid, 256, 0, st>>>(v, M, kernel, bias, prob); break;       \
+        default: head_fwd_bin_kernel<MODE_, 64><<<grid, 256, 0, st>>>(v, M, kernel, bias, prob); break;       \
+    }
+        if (x->mode == UNET_VIEW_BNRELU) {
+            UNET_HB(UNET_VIEW_BNRELU)
+        } else {
+            UNET_HB(UNET_VIEW_PLAIN)
+        }
+#undef UNET_HB
+        UNET_CHECK_LAUNCH("unet_head_fwd");
+        return 0;
+    }
     const int TP = (ncls > 1 ? 4096 : 8192) / x->c0 < 256 ? (ncls > 1 ? 4096 : 8192) / x->c0 : 256;
     int64_t g = cdiv(M, TP);
     const int grid = (int)(g > 4096 ? 4096 : g);

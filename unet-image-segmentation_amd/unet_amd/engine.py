@@ -169,6 +169,8 @@ class UNetEngine:
         # Conv2DTranspose weight / bias gradients on the side stream (its data gradient stays on
         # the critical path); the side stream is otherwise idle until the deferred work is issued
         self.convt_wgrad_side = os.environ.get("UNET_CONVT_SIDE", "1") != "0"
+        # Conv2DTranspose data gradient emits the BN-backward partials of the block below (no pass over da, z)
+        self.convt_bn_stats = os.environ.get("UNET_CONVT_BNSTATS", "1") != "0"
         self._deferred: List = []
         self._held_mark: Optional[int] = None
 
@@ -589,7 +591,27 @@ class UNetEngine:
                 xv = xv.dropout(self.dropout_rate, seeds["bneck_dropout"])
             h, w = self._dims(b1.level + 1)
             gk, gb = self.gvars[f"{stage}_upsample/kernel"], self.gvars[f"{stage}_upsample/bias"]
-            if self.overlap and self.convt_wgrad_side:
+            pb = A.blocks[prev.name]
+            S = 0
+            if self.convt_bn_stats and self.fuse_bn_stats and self.fuse_bn_bwd:
+                S = ops.conv_transpose2x2_bwd_data_bnstats_slabs(xv, n, h, w, fi)
+            if S > 0:
+                need = ops.bn_stats_partials_numel(S, xv.c0)
+                if pb.bnpart is None or pb.bnpart.numel() < need:
+                    pb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
+                ops.conv_transpose2x2_bwd_data_bnstats(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
+                                                       A.dup[stage], pb.da, pb.mean if self.use_bn else None,
+                                                       pb.rstd if self.use_bn else None, pb.bnpart)
+                pb.bn_slabs = S
+                if self.overlap and self.convt_wgrad_side:
+                    self.side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self.side):
+                        ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
+                                                  A.dup[stage], None, gk, gb)
+                else:
+                    ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
+                                              None, gk, gb)
+            elif self.overlap and self.convt_wgrad_side:
                 # data gradient on the critical path, weight + bias gradients on the side stream
                 ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
                                           A.blocks[prev.name].da, None, None)

@@ -435,6 +435,27 @@ def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: O
           _ptr(dk), _ptr(db), ws, wsb, _stream())
 
 
+def conv_transpose2x2_bwd_data_bnstats_slabs(x: View, n, h, w, cout) -> int:
+    """Slab count of conv_transpose2x2_bwd_data_bnstats's BN partials (0: no such path)."""
+    vs = x.c_struct()
+    return L.query("unet_conv_transpose2x2_bwd_data_bnstats_slabs", ctypes.byref(vs), n, h, w, cout)
+
+
+def conv_transpose2x2_bwd_data_bnstats(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Tensor, mean, rstd,
+                                       partials: Tensor):
+    """Data gradient of conv_transpose2x2 (x: the BNRELU view of the block below, no dropout) that
+    also emits that block's BN-backward partials (finish: bn_relu_bwd_stats_finish)."""
+    S = conv_transpose2x2_bwd_data_bnstats_slabs(x, n, h, w, cout)
+    _check(dout, "dout", n * 4 * h * w * cout)
+    _check(dx, "dx", n * h * w * x.c0)
+    _check(partials, "bn_partials", bn_stats_partials_numel(S, x.c0))
+    vs = x.c_struct()
+    m = n * h * w
+    nb = 16.0 * m * cout + 8.0 * m * x.c0 + 16.0 * x.c0 * cout + 8.0 * S * x.c0
+    _call("unet_conv_transpose2x2_bwd_data_bnstats", (8.0 * m * x.c0 * cout, nb), ctypes.byref(vs), n, h, w, cout,
+          _ptr(k), _ptr(dout), _ptr(dx), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
+
+
 # ---------------------------------------------------------------- head / loss ---
 def head_fwd(x: View, n, h, w, ncls, k: Tensor, b: Optional[Tensor], prob: Tensor):
     _check(k, "kernel", x.c0 * ncls)
