@@ -68,6 +68,17 @@ typedef struct unet_view {
 int unet_abi_version(void);
 const char* unet_last_error(void);
 
+/* Cross-stream ordering for a caller that splits the backward over two HIP
+ * streams of one device (the reference has no counterpart: TF schedules its
+ * own graph).  The event carries no timing and only a device-scope release
+ * (hipEventDisableSystemFence): ordering between the streams, not visibility
+ * to the host.  unet_stream_wait_stream records `event` on `producer` and
+ * makes `waiter` wait for it; the event can be reused at once.              */
+int unet_event_create(void** event);
+int unet_event_destroy(void* event);
+int unet_stream_wait_stream(unet_stream_t waiter, unet_stream_t producer,
+                            void* event);
+
 /* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
  * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers
  * read views directly); it serves eager conv_block outputs and inspection.                 */

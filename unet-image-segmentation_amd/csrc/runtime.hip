@@ -164,3 +164,33 @@ int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, i
 
 extern "C" int unet_abi_version(void) { return UNET_ABI_VERSION; }
 extern "C" const char* unet_last_error(void) { return unet::g_err; }
+
+// Cross-stream ordering events for the two-stream backward.  Both streams live on one device, so
+// the device-scope release of a marker is enough: no timing, no system-scope fence (the default
+// event's system-scope writeback/invalidate stalls the recording stream for several us).
+extern "C" int unet_event_create(void** event) {
+    UNET_CHECK_ARG(event, "unet_event_create: null out pointer");
+    hipEvent_t e = nullptr;
+    hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence);
+    if (rc != hipSuccess) {
+        unet::set_error("unet_event_create: %s", hipGetErrorString(rc));
+        return (int)rc;
+    }
+    *event = e;
+    return 0;
+}
+extern "C" int unet_event_destroy(void* event) {
+    if (!event) return 0;
+    return (int)hipEventDestroy(static_cast<hipEvent_t>(event));
+}
+extern "C" int unet_stream_wait_stream(unet_stream_t waiter, unet_stream_t producer, void* event) {
+    UNET_CHECK_ARG(event, "unet_stream_wait_stream: null event");
+    hipEvent_t e = static_cast<hipEvent_t>(event);
+    hipError_t rc = hipEventRecord(e, static_cast<hipStream_t>(producer));
+    if (rc == hipSuccess) rc = hipStreamWaitEvent(static_cast<hipStream_t>(waiter), e, 0);
+    if (rc != hipSuccess) {
+        unet::set_error("unet_stream_wait_stream: %s", hipGetErrorString(rc));
+        return (int)rc;
+    }
+    return 0;
+}

@@ -44,6 +44,9 @@ P = c_void_p
 SIGNATURES = {
     "unet_abi_version": (c_int, []),
     "unet_last_error": (c_char_p, []),
+    "unet_event_create": (c_int, [POINTER(c_void_p)]),
+    "unet_event_destroy": (c_int, [P]),
+    "unet_stream_wait_stream": (c_int, [P, P, P]),
     "unet_view_materialize": (c_int, [_VP, c_int, c_int, c_int, P, P]),
     "unet_dwconv3x3_fwd": (c_int, [_VP, c_int, c_int, c_int, P, P, P]),
     "unet_dwconv3x3_bwd_data": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P]),

@@ -171,6 +171,9 @@ class UNetEngine:
         self.convt_wgrad_side = os.environ.get("UNET_CONVT_SIDE", "1") != "0"
         # Conv2DTranspose data gradient emits the BN-backward partials of the block below (no pass over da, z)
         self.convt_bn_stats = os.environ.get("UNET_CONVT_BNSTATS", "1") != "0"
+        # cross-stream waits through device-scope events (no system-scope fence per marker)
+        self.device_events = os.environ.get("UNET_DEVICE_EVENTS", "1") != "0"
+        self._ev = None  # created on first use (on the device)
         self._deferred: List = []
         self._held_mark: Optional[int] = None
 
@@ -382,6 +385,25 @@ class UNetEngine:
         return A.result
 
     # ----------------------------------------------------------------- backward ------
+    def _event(self):
+        if self._ev is None and self.device_events:
+            self._ev = ops.DeviceEvent()
+        return self._ev
+
+    def _side_wait_main(self):
+        main = torch.cuda.current_stream(self.device)
+        if self._event() is None:
+            self.side.wait_stream(main)
+        else:
+            self._ev.wait(self.side, main)
+
+    def _main_wait_side(self):
+        main = torch.cuda.current_stream(self.device)
+        if self._event() is None:
+            main.wait_stream(self.side)
+        else:
+            self._ev.wait(main, self.side)
+
     def _grads_ready(self, name: str):
         """Gradients at flat offsets >= offset(name) are final once both streams get here:
         the hook (bucketed all-reduce) is issued from the side stream after it has caught up
@@ -391,7 +413,7 @@ class UNetEngine:
                 self._held_mark = self.train_layout.offsets[name]
                 return
             if self.overlap:
-                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                self._side_wait_main()
                 with torch.cuda.stream(self.side):
                     self.grad_hook(self.train_layout.offsets[name])
             else:
@@ -465,7 +487,7 @@ class UNetEngine:
             self._deferred.append((ev, weight_grads))
         elif not chunked:  # (chunked: after all chunks' data gradients, below)
             if self.overlap:  # weight gradients off the critical path, on the side stream
-                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                self._side_wait_main()
                 with torch.cuda.stream(self.side):
                     weight_grads()
             else:
@@ -496,7 +518,7 @@ class UNetEngine:
             if Sc > 0:
                 tb.bn_slabs = K * Sc
             if self.overlap:
-                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                self._side_wait_main()
                 with torch.cuda.stream(self.side):
                     weight_grads()
             else:
@@ -541,7 +563,7 @@ class UNetEngine:
         if self._deferred:
             return
         if self._held_mark is not None and self.grad_hook is not None:
-            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            self._side_wait_main()
             with torch.cuda.stream(self.side):
                 self.grad_hook(self._held_mark)
         self._held_mark = None
@@ -604,7 +626,7 @@ class UNetEngine:
                                                        pb.rstd if self.use_bn else None, pb.bnpart)
                 pb.bn_slabs = S
                 if self.overlap and self.convt_wgrad_side:
-                    self.side.wait_stream(torch.cuda.current_stream(self.device))
+                    self._side_wait_main()
                     with torch.cuda.stream(self.side):
                         ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
                                                   A.dup[stage], None, gk, gb)
@@ -615,7 +637,7 @@ class UNetEngine:
                 # data gradient on the critical path, weight + bias gradients on the side stream
                 ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
                                           A.blocks[prev.name].da, None, None)
-                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                self._side_wait_main()
                 with torch.cuda.stream(self.side):
                     ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
                                               None, gk, gb)
@@ -642,7 +664,7 @@ class UNetEngine:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
         self._flush_deferred()
         if self.overlap:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._main_wait_side()
 
     # --------------------------------------------------------------- train step ------
     def forward_train(self, x: torch.Tensor, y_true: torch.Tensor) -> torch.Tensor:

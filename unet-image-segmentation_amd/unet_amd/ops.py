@@ -26,6 +26,30 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+class DeviceEvent:
+    """Cross-stream ordering event of one device (unet_event_create: no timing, device-scope
+    release only).  wait(waiter, producer) = waiter.wait_stream(producer) without the default
+    event's system-scope fence."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        L.call("unet_event_create", ctypes.byref(h))
+        self._h = h
+
+    def wait(self, waiter, producer):
+        L.call("unet_stream_wait_stream", ctypes.c_void_p(waiter.cuda_stream), ctypes.c_void_p(producer.cuda_stream),
+               self._h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.load().unet_event_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
 def _check(t: Tensor, name: str, numel: Optional[int] = None):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name}: expected a torch.Tensor")
