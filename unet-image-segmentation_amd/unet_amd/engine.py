@@ -173,6 +173,7 @@ class UNetEngine:
         self.convt_bn_stats = os.environ.get("UNET_CONVT_BNSTATS", "1") != "0"
         # cross-stream waits through device-scope events (no system-scope fence per marker)
         self.device_events = os.environ.get("UNET_DEVICE_EVENTS", "1") != "0"
+        self.last_wgrad_main = os.environ.get("UNET_LAST_WGRAD_MAIN", "1") != "0"
         self._ev = None  # created on first use (on the device)
         self._deferred: List = []
         self._held_mark: Optional[int] = None
@@ -486,7 +487,9 @@ class UNetEngine:
             ev.record(torch.cuda.current_stream(self.device))
             self._deferred.append((ev, weight_grads))
         elif not chunked:  # (chunked: after all chunks' data gradients, below)
-            if self.overlap:  # weight gradients off the critical path, on the side stream
+            # the image block (dx0 None) has no data gradient after this: its weight gradients run
+            # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
+            if self.overlap and not (dx0 is None and self.last_wgrad_main):
                 self._side_wait_main()
                 with torch.cuda.stream(self.side):
                     weight_grads()
