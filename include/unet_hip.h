@@ -246,6 +246,23 @@ int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m,
                                    uint64_t drop_seed, float* dy, float* dz,
                                    unet_stream_t stream);
 
+/* The image block (enc1_block1 over the 3-channel input zero-padded to 4):
+ * unet_pointwise_bwd_data_bnrelu without dropout, cin == 4, cout 32 or 64,
+ * that also writes the pointwise kernel gradient d_pw_kernel[ci][co] =
+ * sum_m y[m,ci] dz[m,co] (y: the depthwise output, m x 4) from the dz it forms
+ * on load, so dz is never stored (one streaming pass over da, z, y).
+ * Workspace: _workspace(m, cin, cout) bytes (0: shape not supported).      */
+size_t unet_pointwise_bwd_data_bnrelu_wgrad_workspace(int64_t m, int cin,
+                                                      int cout);
+int unet_pointwise_bwd_data_bnrelu_wgrad(const float* da, const float* z,
+                                         int64_t m, int cin, int cout,
+                                         const float* pw_kernel,
+                                         const float* scale, const float* shift,
+                                         const float* coef, const float* y,
+                                         float* dy, float* d_pw_kernel,
+                                         void* ws, size_t ws_bytes,
+                                         unet_stream_t stream);
+
 /* ----- Conv2DTranspose(f, 2, strides=2, padding='same') — u_net.py:88-94 --
  * out[n, 2i+a, 2j+b, co] = bias[co] + sum_ci x[n,i,j,ci] * k[a,b,co,ci];
  * kernel is Keras (2, 2, Cout, Cin), x a view of (n, h, w, Cin).           */

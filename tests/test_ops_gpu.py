@@ -206,6 +206,45 @@ def test_bn_relu_bwd(ops, use_bn, drop, m, c):
     assert rel_err(host(dz), rz.reshape(m, c)) < 1e-4
 
 
+@pytest.mark.parametrize("use_bn", [True, False])
+@pytest.mark.parametrize("m,cout", [(300, 64), (37, 32), (1000, 32), (40000, 64), (300000, 64)])  # ragged; 2048 slabs
+def test_pointwise_bwd_data_bnrelu_wgrad(ops, use_bn, m, cout):
+    """Image block (cin 4): data gradient plus the pointwise weight gradient from the dz formed on the
+    fly (dz never stored): dy against the GEMM launch, dW against the float64 oracle
+    sum_m y[m, ci] dz[m, co] and against the stored-dz weight-gradient launch."""
+    rng = np.random.default_rng(m + 3 * cout + use_bn)
+    cin, c = 4, cout
+    z = f32(rng.standard_normal((m, c)) * 2 + 0.3)
+    da = f32(rng.standard_normal((m, c)))
+    y = f32(rng.standard_normal((m, cin)))
+    y[:, 3] = 0.0  # the padded image channel
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cout))
+    gamma, beta = bn_affine(rng, c)
+    if use_bn:
+        mean, var = z.mean(0), z.var(0)
+        rstd = 1 / np.sqrt(var + 1e-3)
+        scale, shift = f32(gamma * rstd), f32(beta - mean * gamma * rstd)
+    else:
+        mean = rstd = np.zeros(c)
+        scale, shift = f32(np.ones(c)), beta
+    dg, db, coef = torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"), torch.empty(3 * c, device="cuda")
+    ts, th = dev(scale), dev(shift)
+    ops.bn_relu_bwd_stats(dev(da), dev(z), m, c, dev(f32(mean)), dev(f32(rstd)), ts, th, use_bn, 0.0, 0,
+                          dg if use_bn else None, db, coef)
+    dy_f, dy_p = torch.empty((m, cin), device="cuda"), torch.empty((m, cin), device="cuda")
+    dpk_f, dpk_p = torch.full((1, 1, cin, cout), 7.0, device="cuda"), torch.empty((1, 1, cin, cout), device="cuda")
+    dz = torch.empty((m, c), device="cuda")
+    ops.pointwise_bwd_data_bnrelu_wgrad(dev(da), dev(z), m, cin, cout, dev(pk), ts, th, coef, dev(y), dy_f, dpk_f)
+    assert ops.L.query("unet_pointwise_bwd_data_bnrelu_wgrad_workspace", m, cin, 48) == 0
+    ops.pointwise_bwd_data_bnrelu(dev(da), dev(z), m, cin, cout, dev(pk), ts, th, coef, 0.0, 0, dy_p, dz)
+    assert rel_err(host(dy_f), host(dy_p)) < 1e-5  # (different summation order from the MFMA GEMM)
+    ops.pointwise_bwd_filter(dev(y), dz, m, cin, cout, dpk_p)
+    assert rel_err(host(dpk_f), host(dpk_p)) < 1e-5
+    ref = y.astype(np.float64).T @ host(dz).astype(np.float64)
+    assert rel_err(host(dpk_f).reshape(cin, cout), ref) < 1e-5
+    assert not torch.any(dpk_f[0, 0, 3])  # zero input channel -> zero gradient row
+
+
 @pytest.mark.parametrize("use_bn,drop", [(True, 0.0), (True, 0.2), (False, 0.0)])
 @pytest.mark.parametrize("m,cin,cout", [(300, 16, 32), (1000, 64, 128), (257, 128, 64), (128, 4, 8)])
 def test_pointwise_bwd_data_bnrelu(ops, use_bn, drop, m, cin, cout):

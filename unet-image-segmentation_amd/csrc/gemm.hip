@@ -924,6 +924,109 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         }
 }
 
+// ------------------------------------------------------- image-block data + weight gradient ----
+// The image block's pointwise layer is 4 -> C (C = 4G <= 64): its data gradient dy (M x 4) and
+// weight gradient dW (4 x C) are two thin reductions over the dz it forms from (da, z), so one
+// streaming VALU pass does both (a 4-wide MFMA tile would waste 15/16 of the matrix core): G lanes
+// per pixel (one channel quad each), U pixels in flight per lane; dy by xor shuffles over the G
+// lanes, dW accumulated per lane over its pixels, then over the lanes / waves of the block into
+// one slab per block.
+template <int G>
+__global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                         int64_t M, const float* __restrict__ P,
+                                                         const float* __restrict__ sc, const float* __restrict__ sh,
+                                                         const float* __restrict__ coef, const float* __restrict__ y,
+                                                         float* __restrict__ dy, float* __restrict__ wpart) {
+    constexpr int C = 4 * G, PPW = 64 / G, U = 4, PB = 4 * U * PPW;
+    __shared__ float4 red[4][4][G];  // [wave][ci][quad]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = lane % G, ps = lane / G;
+    const int c = 4 * q;
+    const float4 csc = ld4(sc + c), csh = ld4(sh + c), cmu = ld4(coef + c), cp = ld4(coef + C + c),
+                 cq = ld4(coef + 2 * C + c);
+    float4 pk[4], wacc[4];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+        pk[ci] = ld4(P + ci * C + c);
+        wacc[ci] = f4(0.f);
+    }
+    for (int64_t base = (int64_t)blockIdx.x * PB; base < M; base += (int64_t)gridDim.x * PB) {
+        const int64_t p0 = base + wave * U * PPW + ps;
+        float4 ra[U], rz[U], ry[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t m = p0 + u * PPW;
+            const bool in = m < M;
+            ra[u] = in ? ld4(da + m * C + c) : f4(0.f);
+            rz[u] = in ? ld4(z + m * C + c) : f4(0.f);
+            ry[u] = in ? ld4(y + m * 4) : f4(0.f);
+        }
+        float4 s[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float4 zz = rz[u];
+            float4 v = ra[u];
+            v.x = fmaf(zz.x, csc.x, csh.x) > 0.f ? v.x : 0.f;
+            v.y = fmaf(zz.y, csc.y, csh.y) > 0.f ? v.y : 0.f;
+            v.z = fmaf(zz.z, csc.z, csh.z) > 0.f ? v.z : 0.f;
+            v.w = fmaf(zz.w, csc.w, csh.w) > 0.f ? v.w : 0.f;
+            // dz; for a pixel past M it is not 0, but its y is (dW) and its dy is not stored
+            v.x = csc.x * (v.x - cp.x - (zz.x - cmu.x) * cq.x);
+            v.y = csc.y * (v.y - cp.y - (zz.y - cmu.y) * cq.y);
+            v.z = csc.z * (v.z - cp.z - (zz.z - cmu.z) * cq.z);
+            v.w = csc.w * (v.w - cp.w - (zz.w - cmu.w) * cq.w);
+            s[u].x = v.x * pk[0].x + v.y * pk[0].y + v.z * pk[0].z + v.w * pk[0].w;
+            s[u].y = v.x * pk[1].x + v.y * pk[1].y + v.z * pk[1].z + v.w * pk[1].w;
+            s[u].z = v.x * pk[2].x + v.y * pk[2].y + v.z * pk[2].z + v.w * pk[2].w;
+            s[u].w = v.x * pk[3].x + v.y * pk[3].y + v.z * pk[3].z + v.w * pk[3].w;
+            wacc[0] = fma4(v, f4(ry[u].x), wacc[0]);
+            wacc[1] = fma4(v, f4(ry[u].y), wacc[1]);
+            wacc[2] = fma4(v, f4(ry[u].z), wacc[2]);
+            wacc[3] = fma4(v, f4(ry[u].w), wacc[3]);
+        }
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                s[u].x += __shfl_xor(s[u].x, off, 64);
+                s[u].y += __shfl_xor(s[u].y, off, 64);
+                s[u].z += __shfl_xor(s[u].z, off, 64);
+                s[u].w += __shfl_xor(s[u].w, off, 64);
+            }
+        if (q == 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t m = p0 + u * PPW;
+                if (m < M) st4(dy + m * 4, s[u]);
+            }
+        }
+    }
+    // dW: lanes of one quad (lane % G) in the wave, then the 4 waves, in a fixed order
+#pragma unroll
+    for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            wacc[ci].x += __shfl_xor(wacc[ci].x, off, 64);
+            wacc[ci].y += __shfl_xor(wacc[ci].y, off, 64);
+            wacc[ci].z += __shfl_xor(wacc[ci].z, off, 64);
+            wacc[ci].w += __shfl_xor(wacc[ci].w, off, 64);
+        }
+    if (lane < G) {
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) red[wave][ci][lane] = wacc[ci];
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 * G) {
+        const int ci = threadIdx.x / G, qq = threadIdx.x % G;
+        const float4 t = add4(add4(red[0][ci][qq], red[1][ci][qq]), add4(red[2][ci][qq], red[3][ci][qq]));
+        st4(wpart + (int64_t)blockIdx.x * 4 * C + ci * C + 4 * qq, t);
+    }
+    if (blockIdx.x == gridDim.x - 1) {  // zero slabs up to a multiple of 64 (the two-level reduction)
+        const int S = gridDim.x, Sp = (S + 63) / 64 * 64;
+        for (int i = threadIdx.x; i < (Sp - S) * 4 * C; i += 256) wpart[(int64_t)S * 4 * C + i] = 0.f;
+    }
+}
+
 // ------------------------------------------------------------------------------ launchers ----
 bool rows_vec_ok(const RowsArgs& a, int amode) {
     if (a.K % 4 || a.N % 4) return false;
@@ -1178,6 +1281,53 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
     if (drop_rate > 0.f)
         return launch_rows<A_BNBWD, true, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
     return launch_rows<A_BNBWD, false, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
+}
+
+namespace {
+int img_pw_slabs(int64_t m, int cout) {
+    const int64_t pb = 16 * (64 / (cout / 4));  // pixels per block iteration
+    const int64_t g = cdiv(m, pb);
+    return (int)(g < 2048 ? g : 2048);
+}
+}  // namespace
+
+extern "C" size_t unet_pointwise_bwd_data_bnrelu_wgrad_workspace(int64_t m, int cin, int cout) {
+    if (m <= 0 || cin != 4 || (cout != 32 && cout != 64)) return 0;
+    const int64_t sp = cdiv(img_pw_slabs(m, cout), 64) * 64;  // slabs, padded to 64 groups of sp/64
+    return align_up((size_t)sp * 4 * cout * sizeof(float), 256) +
+           align_up((size_t)(sp / 64) * 4 * cout * sizeof(float), 256);
+}
+
+extern "C" int unet_pointwise_bwd_data_bnrelu_wgrad(const float* da, const float* z, int64_t m, int cin, int cout,
+                                                    const float* pw_kernel, const float* scale, const float* shift,
+                                                    const float* coef, const float* y, float* dy, float* d_pw_kernel,
+                                                    void* ws, size_t ws_bytes, unet_stream_t stream) {
+    UNET_CHECK_ARG(da && z && pw_kernel && scale && shift && coef && y && dy && d_pw_kernel,
+                   "unet_pointwise_bwd_data_bnrelu_wgrad: null pointer");
+    UNET_CHECK_ARG(m > 0 && cin == 4 && (cout == 32 || cout == 64),
+                   "unet_pointwise_bwd_data_bnrelu_wgrad: needs cin == 4 and cout 32 or 64");
+    UNET_CHECK_ARG(fits_i32(m, cout), "unet_pointwise_bwd_data_bnrelu_wgrad: tensor too large");
+    UNET_CHECK_ARG(((uintptr_t)da | (uintptr_t)z | (uintptr_t)coef | (uintptr_t)scale | (uintptr_t)shift |
+                    (uintptr_t)y | (uintptr_t)dy | (uintptr_t)pw_kernel | (uintptr_t)ws) % 16 == 0,
+                   "unet_pointwise_bwd_data_bnrelu_wgrad: operands must be 16-B aligned");
+    const size_t need = unet_pointwise_bwd_data_bnrelu_wgrad_workspace(m, cin, cout);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_pointwise_bwd_data_bnrelu_wgrad: workspace %zu < %zu", ws_bytes,
+                   need);
+    hipStream_t st = as_stream(stream);
+    const int S = img_pw_slabs(m, cout);
+    float* part = static_cast<float*>(ws);
+    if (cout == 64)
+        img_pw_bwd_kernel<16><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, dy, part);
+    else
+        img_pw_bwd_kernel<8><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, dy, part);
+    UNET_CHECK_LAUNCH("unet_pointwise_bwd_data_bnrelu_wgrad");
+    // two fixed-order levels (up to 2048 slabs of 4*cout floats; one level would run on a few blocks):
+    // 64 groups of T = sp/64 slabs -> T slabs, then T -> 1
+    const int64_t L = (int64_t)4 * cout, sp = cdiv(S, 64) * 64, T = sp / 64;
+    float* mid = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)sp * L * sizeof(float), 256));
+    int rc = reduce_slabs(part, 64, T * L, mid, T * L, T * L, st);
+    if (rc) return rc;
+    return reduce_slabs(mid, (int)T, L, d_pw_kernel, L, L, st);
 }
 
 extern "C" size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout) {

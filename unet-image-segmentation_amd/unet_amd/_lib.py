@@ -76,6 +76,9 @@ SIGNATURES = {
                                        c_size_t, P]),
     "unet_pointwise_bwd_data_bnrelu": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, c_float, c_uint64, P, P,
                                                P]),
+    "unet_pointwise_bwd_data_bnrelu_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int]),
+    "unet_pointwise_bwd_data_bnrelu_wgrad": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, P, P, P, c_size_t,
+                                                     P]),
     "unet_conv_transpose2x2_fwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P]),
     "unet_conv_transpose2x2_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_conv_transpose2x2_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),

@@ -174,6 +174,9 @@ class UNetEngine:
         # cross-stream waits through device-scope events (no system-scope fence per marker)
         self.device_events = os.environ.get("UNET_DEVICE_EVENTS", "1") != "0"
         self.last_wgrad_main = os.environ.get("UNET_LAST_WGRAD_MAIN", "1") != "0"
+        # image block (4 padded channels): data and pointwise weight gradient in one streaming pass over
+        # (da, z, y) that forms dz on the fly, so dz (M x 64) is neither stored nor re-read
+        self.img_fused_wgrad = os.environ.get("UNET_IMG_WGRAD", "1") != "0"
         self._ev = None  # created on first use (on the device)
         self._deferred: List = []
         self._held_mark: Optional[int] = None
@@ -449,6 +452,8 @@ class UNetEngine:
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
             wdz = self.wgrad_forms_dz and drop_rate == 0.0
+            img_wg = (self.img_fused_wgrad and not wdz and drop_rate == 0.0 and b.cin == 4
+                      and b.cout in (32, 64))
             chunked = (self.l0_chunks > 1 and b.level == 0 and dx0 is not None and not wdz and drop_rate == 0.0
                        and view_in.drop_rate == 0.0 and n % self.l0_chunks == 0 and not self.fuse_dw_bwd)
             if chunked:  # chunk 0 only; the others are interleaved with the depthwise data gradient below
@@ -456,11 +461,14 @@ class UNetEngine:
                 ops.pointwise_bwd_data_bnrelu(bb.da[:nc], bb.z[:nc], nc * h * w, b.cin, b.cout, pk, bb.scale,
                                               bb.shift, bb.coef, 0.0, 0, dy.view(n, h, w, b.cin)[:nc],
                                               dz.view(n, h, w, b.cout)[:nc])
+            elif img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
+                ops.pointwise_bwd_data_bnrelu_wgrad(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
+                                                    bb.y, dy, self._gwts(b)[1])
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, None if wdz else dz)
         else:
-            wdz = chunked = False
+            wdz = chunked = img_wg = False
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
@@ -470,7 +478,9 @@ class UNetEngine:
                     and ops.dwconv3x3_bwd_slabs(view_in, n, h, w) > 0)
 
         def weight_grads():
-            if wdz:
+            if img_wg:
+                pass  # already accumulated by the data-gradient GEMM
+            elif wdz:
                 ops.pointwise_bwd_filter_bnrelu(bb.y, bb.da, bb.z, m, b.cin, b.cout, bb.scale, bb.shift, bb.coef, gpk)
             else:
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)

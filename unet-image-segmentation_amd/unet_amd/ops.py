@@ -430,6 +430,24 @@ def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int
           int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream())
 
 
+def pointwise_bwd_data_bnrelu_wgrad(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
+                                    shift: Tensor, coef: Tensor, y: Tensor, dy: Tensor, dpk: Tensor):
+    """pointwise_bwd_data_bnrelu (no dropout) for cin == 4 that also writes the pointwise weight
+    gradient dpk[ci][co] = sum_m y[m, ci] dz[m, co] from the dz it forms (dz is not stored)."""
+    _check(da, "da", m * cout)
+    _check(z, "z", m * cout)
+    _check(pk, "pointwise_kernel", cin * cout)
+    _check(coef, "coef", 3 * cout)
+    _check(y, "y", m * cin)
+    _check(dy, "dy", m * cin)
+    _check(dpk, "d_pointwise_kernel", cin * cout)
+    ws, wsb = _ws(L.query("unet_pointwise_bwd_data_bnrelu_wgrad_workspace", m, cin, cout), da.device)
+    _call("unet_pointwise_bwd_data_bnrelu_wgrad",
+          (4.0 * m * cin * cout, 4.0 * (2 * m * cout + 2 * m * cin + 2 * cin * cout)),
+          _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), _ptr(y), _ptr(dy),
+          _ptr(dpk), ws, wsb, _stream())
+
+
 # ------------------------------------------------------------ Conv2DTranspose ---
 def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor], out: Tensor):
     _check(k, "kernel", 4 * cout * x.c0)
