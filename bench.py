@@ -146,6 +146,17 @@ def pmc_traffic(op):
     return None, None
 
 
+def workload_config(args):
+    """The BASELINE.json config whose per-GPU shape this run measures."""
+    if args.size == 256 and args.num_classes == 1 and args.batch == 16:
+        return "configs[1]"
+    if args.size == 512 and args.num_classes == 1 and args.batch == 8:
+        return "configs[3] (per-GPU shape)"
+    if args.size == 256 and args.num_classes == 21 and args.batch == 8:
+        return "configs[4] (per-GPU shape, batch 32 over 4 GPUs)"
+    return "custom"
+
+
 def synthetic_batch(n, h, w, ncls, seed, device):
     import numpy as np
     import torch
@@ -275,8 +286,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (x~U[0,1) NHWC, quad masks ~30% fg), random-init Keras-glorot weights",
-            "config": {"workload": f"configs[1]: {args.size}x{args.size}x3 binary U-Net train step "
-                                   f"(fwd + dice_loss + bwd + AdamW, dropout 0.2)",
+            "config": {"workload": f"{workload_config(args)}: {args.size}x{args.size}x3 "
+                                   f"{'binary' if args.num_classes == 1 else f'{args.num_classes}-class'} U-Net train "
+                                   f"step (fwd + dice_loss + bwd + AdamW, dropout 0.2)",
                        "model": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                        "seq_len": args.size * args.size, "parallelism": f"dp{world}"},

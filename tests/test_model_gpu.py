@@ -211,6 +211,36 @@ def test_full_size_train_steps_cfg2():
     assert miou.confusion_matrix().sum() == 6 * 16 * 256 * 256
 
 
+@pytest.mark.parametrize("size,batch,ncls", [(512, 8, 1),    # configs[3]: 512x512 binary, batch 8 per GPU
+                                             (256, 8, 21)])  # configs[4]: 21 classes, batch 32 over 4 GPUs
+def test_full_size_train_steps_other_configs(size, batch, ncls):
+    """The per-GPU shapes of BASELINE configs[3] and configs[4]: finite steps whose loss falls on a
+    fixed batch, dice = 1 - loss, probabilities a distribution, confusion counts cover every pixel."""
+    from unet_amd.model import UNetModel
+    from unet_amd.metrics import MeanIoU
+    from unet_amd.optim import AdamW
+    rng = np.random.default_rng(size + ncls)
+    x, y = _data(rng, batch, size, size, ncls)
+    m = UNetModel((size, size, 3), ncls)
+    miou = MeanIoU(2)
+    m.compile(AdamW(2e-3, 1e-4), "dice_loss", [miou, "dice_coef"] if ncls == 1 else ["dice_coef"])
+    losses = []
+    for _ in range(4):
+        r = m.train_step(x, y).cpu().numpy()
+        assert np.isfinite(r).all()
+        assert abs(r[0] + r[1] - 1) < 1e-6
+        losses.append(r[0])
+    assert losses[-1] < losses[0]
+    p = m.predict(x[:1])
+    assert p.shape == (1, size, size, ncls) and p.min() >= 0 and p.max() <= 1
+    if ncls > 1:
+        assert np.abs(p.sum(-1) - 1).max() < 1e-5
+    if ncls == 1:
+        assert miou.confusion_matrix().sum() == 4 * batch * size * size
+    del m
+    torch.cuda.empty_cache()
+
+
 def test_meaniou_metric_api():
     from unet_amd.metrics import MeanIoU
     from oracle import keras_ops as K
