@@ -294,6 +294,7 @@ struct WgradArgs {
     float* slab;  // [S][P][Q]
     const float* bz;     // W_BNBWD: raw z (same layout as b.src0)
     const float* bcoef;  // W_BNBWD: (mu, p, q) x Q
+    float* colpart;      // optional [S][P]: column sums of A over the block's m slice (vectorised kernel, q-tile 0)
 };
 
 template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
@@ -869,9 +870,15 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
             rb[r] = v;
         }
     };
+    const bool csum_on = g.colpart != nullptr && (int)blockIdx.x < ntp;  // q-tile 0 blocks sum A's columns
+    float4 csum = f4(0.f);
     auto store_stage = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[buf][(amm + AS * r) * LDA + 4 * apq]) = ra[r];
+        if (csum_on) {
+#pragma unroll
+            for (int r = 0; r < AR; ++r) csum = add4(csum, ra[r]);
+        }
 #pragma unroll
         for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[buf][(bmm + BS * r) * LDB + 4 * bqq]) = rb[r];
     };
@@ -908,6 +915,16 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         }
         if (kt + 1 < nk) store_stage(buf ^ 1);
         __syncthreads();
+    }
+    if (csum_on) {  // fixed-order sum over the AS m-rows of each column quad (the loop ended on a barrier)
+        float4* T = reinterpret_cast<float4*>(&As[0][0]);
+        T[tid] = csum;
+        __syncthreads();
+        if (tid < PQ && pv) {
+            float4 t = T[tid];
+            for (int j = 1; j < AS; ++j) t = add4(t, T[j * PQ + tid]);
+            st4(g.colpart + (int64_t)blockIdx.y * g.P + p, t);
+        }
     }
     float* slab = g.slab + (int64_t)blockIdx.y * g.P * g.Q;
 #pragma unroll
@@ -1402,10 +1419,22 @@ extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int 
     return launch_rows<A_BNRELU, false, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
 }
 
+namespace {
+bool convt_fused_bias() {  // UNET_CONVT_FUSED_BIAS=0: separate colsum pass (A/B switch)
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("UNET_CONVT_FUSED_BIAS");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+}  // namespace
+
 extern "C" size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int cin, int cout) {
     if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return 0;
     const int64_t M = (int64_t)n * h * w;
-    size_t a = wgrad_workspace(M, 4 * cout, cin);
+    const WgradPlan wp = wgrad_plan(M, 4 * cout, cin);
+    size_t a = wgrad_workspace(M, 4 * cout, cin) + align_up((size_t)wp.S * 4 * cout * sizeof(float), 256);
     size_t b = colsum_workspace(4 * M, cout);
     return a > b ? a : b;
 }
@@ -1454,9 +1483,18 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
     wa.b = make_dview(*x);
     wa.Q = cin;
     wa.M = M;
+    // bias gradient: the q-tile-0 blocks of the kernel-gradient GEMM also sum dU' over their m slice
+    // ([S][4][cout] after the slabs), so dU' is read once; = one fixed-order reduction of 4S rows
+    const WgradPlan wp = wgrad_plan(M, 4 * cout, cin);
+    const size_t slab_bytes = align_up((size_t)wp.S * 4 * cout * cin * sizeof(float), 256);
+    const bool fuse_bias = convt_fused_bias() && cin % 4 == 0 && cout % 4 == 0 &&
+                           ((uintptr_t)dout | (uintptr_t)x->src0) % 16 == 0 &&
+                           ws_bytes >= slab_bytes + (size_t)wp.S * 4 * cout * sizeof(float);
+    if (fuse_bias) wa.colpart = reinterpret_cast<float*>(static_cast<char*>(ws) + slab_bytes);
     int rc = run_wgrad(wa, W_UNSHUFFLE, x->mode == UNET_VIEW_BNRELU ? W_BNRELU : W_PLAIN, dkernel, ws, ws_bytes, st,
                        "unet_conv_transpose2x2_bwd(filter)");
     if (rc) return rc;
+    if (fuse_bias) return reduce_slabs(wa.colpart, 4 * wp.S, cout, dbias, cout, cout, st);
     return colsum(dout, 4 * M, cout, dbias, ws, ws_bytes, st);
 }
 
