@@ -341,6 +341,7 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
                                                            int use_bn, const float* mean, const float* rstd,
                                                            float* dgamma, float* dbeta, float* coef,
                                                            double* chunks, unsigned* cnt) {
+    main_stream_prio();
     const int q = threadIdx.x % kLQ, g = threadIdx.x / kLQ;
     const int c = (blockIdx.x * kLQ + q) * 4;
     const int nch = gridDim.y;

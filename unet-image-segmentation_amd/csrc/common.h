@@ -40,6 +40,16 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Wave issue priority of the critical-path (main-stream) backward kernels: while the weight
+// gradients run beside them on a second stream, their waves win the SIMD's instruction
+// arbitration (s_setprio; 0 = the default, equal priority).  Build-time choice (UNET_MAIN_PRIO).
+#ifndef UNET_MAIN_PRIO
+#define UNET_MAIN_PRIO 0
+#endif
+__device__ __forceinline__ void main_stream_prio() {
+    if constexpr (UNET_MAIN_PRIO > 0) __builtin_amdgcn_s_setprio(UNET_MAIN_PRIO);
+}
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 __device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }

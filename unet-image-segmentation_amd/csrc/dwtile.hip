@@ -183,6 +183,7 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
                                                         const float* __restrict__ mu = nullptr,
                                                         const float* __restrict__ rs = nullptr,
                                                         float* __restrict__ bnpart = nullptr) {
+    main_stream_prio();
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
     int n, h0, w0;

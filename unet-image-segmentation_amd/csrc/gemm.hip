@@ -437,6 +437,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
 // ds_read_b128 of its row.  Row stride BK+4 floats makes those reads conflict-free.
 template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC>
 __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
+    main_stream_prio();
     constexpr int LR = BK + 4;     // A (and k-contiguous B) LDS row stride, floats
     constexpr int LB = BN + 4;     // k-major B LDS row stride (n-contiguous weights)
     constexpr int KQ = BK / 4;
@@ -954,6 +955,7 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ sc, const float* __restrict__ sh,
                                                          const float* __restrict__ coef, const float* __restrict__ y,
                                                          float* __restrict__ dy, float* __restrict__ wpart) {
+    main_stream_prio();
     constexpr int C = 4 * G, PPW = 64 / G, U = 4, PB = 4 * U * PPW;
     __shared__ float4 red[4][4][G];  // [wave][ci][quad]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int6
                                                         float* __restrict__ part_b, const float* __restrict__ mu = nullptr,
                                                         const float* __restrict__ rs = nullptr,
                                                         float* __restrict__ bnpart = nullptr) {
+    main_stream_prio();
     __shared__ float dls[256];
     __shared__ float4 red[256];
     const int Cin = v.c0, CQ = Cin / 4;
