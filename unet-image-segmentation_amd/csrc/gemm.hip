@@ -1076,8 +1076,13 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
         if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
         return RowsCfg{128, 32};
     }
+    static int bk32_k = -1;  // smallest K that takes BK = 32 (UNET_BK32_MIN_K: tuning)
+    if (bk32_k < 0) {
+        const char* e = getenv("UNET_BK32_MIN_K");
+        bk32_k = e ? atoi(e) : 256;
+    }
     if (a.N <= 64) return RowsCfg{64, 16};
-    return RowsCfg{128, a.K >= 256 && amode != A_UNSHUFFLE ? 32 : 16};
+    return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
 template <int BN, int BKk, int AMODE, bool DROP, int EPI>
