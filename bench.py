@@ -8,9 +8,13 @@ configs[1] (batch 16 per GPU, binary, dice loss).  Weak scaling: 16 images per G
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel, timed with HIP events
-on its launch stream over the timed region; `cpu_baseline` is the NumPy oracle train step
-(oracle/unet_ref.py) on a bounded sample, rank 0, N=1 only.
+The step is the reference's `model.fit` step as scripts/train.py:227-234 compiles it: forward,
+dice_loss, backward, AdamW and the MeanIoU(2) + dice_coef metric updates.
+
+Prints ONE JSON line on rank 0.  The timed region records nothing.  `roofline` is for the
+dominant kernel, timed with HIP events on its launch stream over a second pass of the same K
+steps; `cpu_baseline` is the torch-CPU restatement of the same train step (oracle/torch_ref.py,
+SURVEY.md 8(d)'s TF-CPU proxy) on a bounded sample, rank 0, N=1 only.
 """
 from __future__ import annotations
 
@@ -173,31 +177,22 @@ def synthetic_batch(n, h, w, ncls, seed, device):
     return torch.from_numpy(x).to(device), torch.from_numpy(y).to(device)
 
 
-def cpu_baseline(size, ncls, n_img=2):
-    """NumPy oracle train step (float32), batch 1, n_img steps; img/s."""
-    import numpy as np
-    from oracle.unet_ref import UNetOracle
+def cpu_baseline(size, ncls, batch):
+    """SURVEY.md 8(d)'s TF-CPU proxy: the torch-CPU (oneDNN, channels_last, float32) restatement
+    of the identical train step (oracle/torch_ref.py: forward, dice_loss, backward, Keras AdamW,
+    MeanIoU update) on the host cores, a bounded sample of the same workload (>= 10 s)."""
+    from oracle.torch_ref import cpu_info, time_train_steps
     from unet_amd.params import init_weights, unet_variables
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = 1
-    specs = unet_variables(3, ncls)
-    p = init_weights(specs, 1)
-    opt = {s.name: (np.zeros(s.shape, np.float32), np.zeros(s.shape, np.float32)) for s in specs if s.trainable}
-    o = UNetOracle(ncls, 0.2)
-    seeds = {s: i for i, s in enumerate(("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout"))}
-    rng = np.random.default_rng(0)
-    t0 = time.perf_counter()
-    for i in range(n_img):
-        x = rng.random((1, size, size, 3), dtype=np.float32)
-        y = (rng.random((1, size, size, ncls)) > 0.5).astype(np.float32)
-        _, _, _, p, opt, _ = o.train_step(p, opt, x, y, i + 1, 2e-3, 1e-4, drop_seeds=seeds)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_img / dt, 4), "unit": "images/sec", "cores": int(threads), "kind": "port",
-            "sample": f"{n_img} train steps of batch 1 at {size}x{size}x3 (NumPy oracle, float32, "
-                      f"forward+dice+backward+AdamW) on the host CPU"}
+    w = init_weights(unet_variables(3, ncls), 2301)
+    r = time_train_steps(w, size, batch, ncls, min_seconds=10.0, max_steps=4)
+    info = cpu_info()
+    return {"value": r["value"], "unit": "images/sec", "cores": r["threads"], "kind": "port",
+            "impl": "torch-CPU restatement of the TF-CPU reference path (oneDNN, channels_last, fp32)",
+            "cpu_model": info["cpu_model"], "machine_physical_cores": info["machine_physical_cores"],
+            "affinity_cpus": info["affinity_cpus"],
+            "sample": f"{r['steps']} train steps of batch {batch} at {size}x{size}x3 after 1 warm-up step "
+                      f"({r['seconds']} s; forward + dice_loss + backward + AdamW + MeanIoU update), "
+                      f"{r['threads']} threads"}
 
 
 def main():
@@ -218,6 +213,7 @@ def main():
     import torch.distributed as dist
     from unet_amd import ops
     from unet_amd.dp import init_from_env
+    from unet_amd.metrics import MeanIoU
     from unet_amd.model import UNetModel
     from unet_amd.optim import AdamW
 
@@ -225,7 +221,10 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     model = UNetModel((args.size, args.size, 3), args.num_classes, dropout_rate=0.2, device=device)
-    model.compile(AdamW(learning_rate=2e-3, weight_decay=1e-4), "dice_loss")
+    # as scripts/train.py:227-234 compiles it: dice_loss, metrics MeanIoU(2) + dice_coef, so the
+    # MeanIoU confusion update runs inside every timed step
+    model.compile(AdamW(learning_rate=2e-3, weight_decay=1e-4), "dice_loss",
+                  metrics=[MeanIoU(num_classes=2, name="mean_io_u", device=device), "dice_coef"])
     if world > 1:
         model.enable_data_parallel()
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
@@ -238,11 +237,9 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # one untimed single-stream step with every C-ABI op bracketed by HIP events: per-op
-    # breakdown, and the dominant op whose launches the timed region then measures (on the
-    # stream each launch is issued on) for the roofline object
+    # per-op breakdown: one untimed single-stream step with every C-ABI op bracketed by HIP
+    # events on its launch stream; its largest op is the one the roofline object reports
     breakdown, dominant = None, ROOFLINE_OP
-    timer = None
     if not args.no_roofline:
         bt = ops.KernelTimer(None)
         ops.TIMER = bt
@@ -253,8 +250,8 @@ def main():
         ops.TIMER = None
         breakdown = op_breakdown(bt.summary())
         dominant = breakdown[0]["op"]
-        timer = ops.KernelTimer([dominant])
-        ops.TIMER = timer
+
+    # the timed region: K steps, nothing recorded inside it
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -263,12 +260,25 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    ops.TIMER = None
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(res[0].item())
+
+    # roofline pass: the same K steps again (same streams, same overlap) with the dominant
+    # kernel's launches bracketed by HIP events on the stream each is issued on
+    timer, dt_roof = None, None
+    if not args.no_roofline:
+        timer = ops.KernelTimer([dominant])
+        ops.TIMER = timer
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            model.train_step(x, y)
+        torch.cuda.synchronize()
+        dt_roof = time.perf_counter() - t1
+        ops.TIMER = None
 
     out = None
     if rank == 0:
@@ -288,8 +298,8 @@ def main():
             "data": "synthetic (x~U[0,1) NHWC, quad masks ~30% fg), random-init Keras-glorot weights",
             "config": {"workload": f"{workload_config(args)}: {args.size}x{args.size}x3 "
                                    f"{'binary' if args.num_classes == 1 else f'{args.num_classes}-class'} U-Net train "
-                                   f"step (fwd + dice_loss + bwd + AdamW, dropout 0.2)",
-                       "model": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
+                                   f"step (fwd + dice_loss + bwd + AdamW + MeanIoU(2) update, dropout 0.2)",
+                       "network": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                        "seq_len": args.size * args.size, "parallelism": f"dp{world}"},
             "final_loss": round(loss, 6),
@@ -298,13 +308,17 @@ def main():
             s = timer.summary().get(dominant)
             if s:
                 out["roofline"] = roofline_obj(dominant, s, args.steps)
+                out["roofline"]["timing"] = (f"separate pass of {args.steps} steps after the timed region "
+                                             f"({dt_roof / args.steps * 1e3:.3f} ms/step with events)")
                 out["op_breakdown"] = breakdown[:8]
+        if model.mean_iou is not None:
+            out["mean_io_u"] = round(model.mean_iou.result(), 6)
         if not args.no_roofline and world == 1 and args.encoder_batch > 0:
             del model
             torch.cuda.empty_cache()
             out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes)
+            out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes, args.batch)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -5,7 +5,13 @@ regenerated bit-for-bit; outputs are float64 oracle results stored as float32/fl
 The reference itself ships no golden data and cannot run here (TensorFlow absent), so these
 fixtures freeze the oracle (parity unpinned against TF), they do not pin it.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [fixture.npz ...]
+
+The BASELINE-size fixtures (fwd256/fwd512/fwd21/samples/train128) hold the configs[1], [3] and
+[4] geometries at inference and one train step at 128x128 batch 4; samples/ holds the two
+images of the reference's samples/test_images (input data) and, under samples/usage, the
+reference's own inference outputs for them (samples/usage/*: output_mask.png,
+output_cropped.png), which pin the post-processing crop (tests/test_imageproc.py).
 """
 import os
 import sys
@@ -105,7 +111,100 @@ def train_fixture():
     return out
 
 
-if __name__ == "__main__":
+FULL = (64, 128, 256, 512)
+
+
+def quad_masks(n, h, w, ncls=1):
+    """Deterministic ID-card-like axis-aligned quads (about 30 % foreground) per image."""
+    y = np.zeros((n, h, w, 1), np.float64)
+    for i in range(n):
+        u = portable_uniform(900 + i, 4)
+        hh, ww = int(h * (0.4 + 0.3 * u[0])), int(w * (0.4 + 0.3 * u[1]))
+        y0, x0 = int(u[2] * (h - hh)), int(u[3] * (w - ww))
+        y[i, y0:y0 + hh, x0:x0 + ww] = 1.0
+    return y
+
+
+def fwd256_fixture():
+    """configs[1] geometry (256x256x3, binary) inference forward on 2 images."""
+    w = model_weights(1, FULL, 2301)
+    x = U(31, (2, 256, 256, 3))
+    prob, _, _ = UNetOracle(1).forward(w, x, training=False)
+    return {"x_seed": 31, "w_seed": 2301, "prob": prob.astype(np.float32)}
+
+
+def fwd512_fixture():
+    """configs[3] geometry (512x512x3, binary) inference forward on 1 image."""
+    w = model_weights(1, FULL, 2301)
+    x = U(32, (1, 512, 512, 3))
+    prob, _, _ = UNetOracle(1).forward(w, x, training=False)
+    return {"x_seed": 32, "w_seed": 2301, "prob": prob.astype(np.float32)}
+
+
+def fwd21_fixture():
+    """configs[4] geometry (256x256x3, 21 classes, softmax head) inference forward on 2 images:
+    probabilities on every 4th pixel, the full argmax map and per-(image, class) sums."""
+    w = model_weights(21, FULL, 2302)
+    x = U(33, (2, 256, 256, 3))
+    prob, _, _ = UNetOracle(21).forward(w, x, training=False)
+    return {"x_seed": 33, "w_seed": 2302, "prob_s4": prob[:, ::4, ::4, :].astype(np.float32),
+            "argmax": prob.argmax(-1).astype(np.uint8), "class_sums": prob.sum((1, 2))}
+
+
+def samples_fixture():
+    """The reference's samples/test_images/*.png through the inference preprocessing
+    (scripts/inference.py:98-110: BGR, /255, INTER_LINEAR to 256x256; restated in
+    scripts/inference.py here) and the forward of the 2301-seeded weights."""
+    sys.path.insert(0, os.path.join(ROOT, "unet-image-segmentation_amd", "scripts"))
+    import inference  # the drop-in CLI module (its preprocessing)
+    w = model_weights(1, FULL, 2301)
+    out = {"w_seed": 2301}
+    for name in SAMPLE_NAMES:
+        x, bgr, h, wd = inference.load_and_preprocess_image(os.path.join(HERE, "samples", name + ".png"), 256, 256)
+        prob, _, _ = UNetOracle(1).forward(w, x.astype(np.float64), training=False)
+        out[name + ":x_sum"] = float(x.astype(np.float64).sum())
+        out[name + ":x_s8"] = x[:, ::8, ::8, :]
+        out[name + ":prob"] = prob.astype(np.float32)
+    return out
+
+
+SAMPLE_NAMES = ("brazil_passport", "chile_id_card")
+
+
+def train128_fixture():
+    """One train step (dropout 0) at 128x128, batch 4, full widths: loss, dice, every gradient's
+    norm and first 128 values, the first 256 post-AdamW values and moving statistics of every
+    variable."""
+    w = model_weights(1, FULL, 11)
+    x = U(41, (4, 128, 128, 3))
+    y = quad_masks(4, 128, 128)
+    orc = UNetOracle(1, 0.0)
+    opt = {k: (np.zeros_like(v), np.zeros_like(v)) for k, v in w.items() if "moving" not in k}
+    loss, dice, g, newp, _, prob = orc.train_step(w, opt, x, y, 1, 2e-3, 1e-4)
+    out = {"x_seed": 41, "w_seed": 11, "loss": loss, "dice": dice}
+    for k, v in g.items():
+        out["gnorm:" + k] = np.linalg.norm(v)
+        out["g128:" + k] = v.reshape(-1)[:128]
+    for k, v in newp.items():
+        out["new256:" + k] = v.reshape(-1)[:256]
+    return out
+
+
+def write(name, d):
+    np.savez_compressed(os.path.join(HERE, name), **{k.replace("/", "|"): v for k, v in d.items()})
+
+
+BIG = {"fwd256.npz": fwd256_fixture, "fwd512.npz": fwd512_fixture, "fwd21.npz": fwd21_fixture,
+       "samples.npz": samples_fixture, "train128.npz": train128_fixture}
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:  # regenerate only the named fixtures
+    for nm in sys.argv[1:]:
+        write(nm, BIG[nm]())
+        print(nm, os.path.getsize(os.path.join(HERE, nm)))
+elif __name__ == "__main__":
+    for nm, fn in BIG.items():
+        write(nm, fn())
     np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops_fixture())
     np.savez_compressed(os.path.join(HERE, "cfg1_forward.npz"), **cfg1_fixture())
     tf = train_fixture()

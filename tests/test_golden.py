@@ -40,6 +40,19 @@ def test_oracle_reproduces_train_golden():
         assert np.allclose(new[k], v, rtol=1e-9, atol=1e-15), k
 
 
+@pytest.mark.parametrize("name", sorted(MG.BIG))
+def test_oracle_reproduces_baseline_size_goldens(name):
+    """The BASELINE-geometry fixtures (fwd256/fwd512/fwd21/samples/train128) are reproduced by
+    the oracle (float64 rounding only)."""
+    g = _load(name)
+    new = {k.replace("|", "/"): v for k, v in MG.BIG[name]().items()}
+    assert set(g) == set(new)
+    for k, v in g.items():
+        a, b = np.asarray(new[k], np.float64), np.asarray(v, np.float64)
+        assert a.shape == b.shape, k
+        assert np.allclose(a, b, rtol=1e-9, atol=1e-12), k
+
+
 @pytest.mark.gpu
 def test_hip_matches_cfg1_golden():
     """configs[0] through the reference builder API: masks within 1e-3 of the golden output."""

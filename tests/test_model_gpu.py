@@ -9,6 +9,9 @@ Tolerances (north star: masks within 1e-3 on identical weights/inputs):
     few samples at small test sizes amplifies rounding to ~1e-3..1e-2 in some gradients);
     post-AdamW weights within 1e-4 relative.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -114,7 +117,7 @@ def test_builder_api_and_inference_parity_cfg1():
                                                         (1, True, 0.2, "dice_loss", "always"),
                                                         (1, True, 0.2, "dice_loss", "chunked"),
                                                         (1, False, 0.0, "dice_loss", "chunked")])
-def test_train_step_parity(ncls, use_bn, drop, loss, fuse):
+def test_train_step_parity(ncls, use_bn, drop, loss, fuse, record_property):
     """One train step against the oracle; fuse="always" runs the fused depthwise+pointwise
     forward on every level it supports (32x32 and 16x16 here), "never" the split kernels;
     "chunked" runs the top level's backward GEMM / depthwise data gradient in 2 batch chunks."""
@@ -146,6 +149,14 @@ def test_train_step_parity(ncls, use_bn, drop, loss, fuse):
             break
     else:
         pytest.fail("no inputs found whose ReLU / max-pool decisions are not decided by rounding")
+    # how many input draws it took to find one whose discrete decisions all agree with fp64
+    record_property("input_draws", attempt + 1)
+    print(f"train_step_parity[{ncls},{use_bn},{drop},{loss},{fuse}]: input draws = {attempt + 1}")
+    log = os.environ.get("UNET_PARITY_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": f"train_step_parity[{ncls},{use_bn},{drop},{loss},{fuse}]",
+                                "input_draws": attempt + 1}) + "\n")
     assert abs(res[0] - lval) < 1e-5, (res[0], lval)
     assert abs(res[1] - dice) < 1e-5
     # fp32 conditioning reference: the same oracle step in float32

@@ -1,0 +1,182 @@
+"""Parity of the MI355X engine with the oracle at the BASELINE.json geometries (not toy sizes).
+
+  * configs[1] geometry, 256x256x3 binary, inference on 2 images   (tests/golden/fwd256.npz)
+  * configs[3] geometry, 512x512x3 binary, inference on 1 image    (fwd512.npz)
+  * configs[4] geometry, 256x256x3, 21 classes, inference on 2     (fwd21.npz)
+  * the reference's samples/test_images/*.png through scripts/inference.py's preprocessing
+    (BGR, /255, INTER_LINEAR, reference scripts/inference.py:98-110)  (samples.npz)
+  * one train step at 128x128, batch 4, full widths, against the float64 oracle run live on
+    the host (every gradient tensor) and against the committed golden (norms, slices, AdamW)
+
+Tolerances (north star: masks within 1e-3 on identical weights and inputs):
+  * probabilities: max |p - p_ref| < 1e-3 (the bar), and < 5e-5 (what fp32 rounding gives);
+  * binary masks at the 0.5 threshold (scripts/inference.py:160) identical wherever
+    |p_ref - 0.5| > 1e-4; 21-class argmax identical wherever the top-2 margin > 1e-4;
+  * train step: loss and dice within 1e-5; each gradient tensor within relative L2
+    max(2e-3, 2 e32) of the float64 oracle, e32 = the same oracle step run in float32 (its own
+    distance to float64).  ReLU / max-pool decisions that sit within fp32 rounding of their
+    boundary flip between any fp32 run and fp64 (10 of 5.9 M at this size); they are counted
+    and logged, not re-drawn away.  Post-AdamW values within 1e-4; gradient norms within 1e-2.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import host, norm_err
+from oracle.unet_ref import UNetOracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, HERE)
+import make_golden as MG  # noqa: E402
+
+LOG = os.environ.get("UNET_PARITY_LOG")
+
+
+def _log(rec):
+    print(json.dumps(rec))
+    if LOG:
+        with open(LOG, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
+def _load(name):
+    with np.load(os.path.join(HERE, name), allow_pickle=False) as z:
+        return {k.replace("|", "/"): z[k] for k in z.files}
+
+
+def _model(size, ncls, w_seed):
+    from model.u_net import U_NET
+    m = U_NET((size, size, 3), ncls)
+    w = MG.model_weights(ncls, MG.FULL, int(w_seed))
+    m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+    return m
+
+
+def _check_binary(prob, ref, name):
+    err = float(np.abs(prob.astype(np.float64) - ref.astype(np.float64)).max())
+    far = np.abs(ref - 0.5) > 1e-4
+    agree = np.array_equal((prob > 0.5)[far], (ref > 0.5)[far])
+    _log({"test": name, "max_abs_err": err, "masks_agree": bool(agree), "pixels": int(ref.size)})
+    assert err < 1e-3
+    assert err < 5e-5
+    assert agree
+
+
+@pytest.mark.parametrize("fixture,size,n", [("fwd256.npz", 256, 2), ("fwd512.npz", 512, 1)])
+def test_inference_binary_baseline_geometry(fixture, size, n):
+    g = _load(fixture)
+    m = _model(size, 1, g["w_seed"])
+    x = MG.U(int(g["x_seed"]), (n, size, size, 3)).astype(np.float32)
+    prob = m.predict(x)
+    assert prob.shape == (n, size, size, 1)
+    _check_binary(prob, g["prob"], fixture)
+    del m
+    torch.cuda.empty_cache()
+
+
+def test_inference_21_classes():
+    g = _load("fwd21.npz")
+    m = _model(256, 21, g["w_seed"])
+    x = MG.U(int(g["x_seed"]), (2, 256, 256, 3)).astype(np.float32)
+    prob = m.predict(x).astype(np.float64)
+    err = float(np.abs(prob[:, ::4, ::4, :] - g["prob_s4"]).max())
+    srt = np.sort(prob, -1)
+    margin = srt[..., -1] - srt[..., -2]
+    sure = margin > 1e-4
+    agree = np.array_equal(prob.argmax(-1)[sure], g["argmax"][sure])
+    sums_err = float(np.abs(prob.sum((1, 2)) - g["class_sums"]).max() / np.abs(g["class_sums"]).max())
+    _log({"test": "fwd21", "max_abs_err_s4": err, "argmax_agree": bool(agree), "class_sums_rel": sums_err})
+    assert err < 1e-3 and err < 5e-5
+    assert agree
+    assert sums_err < 1e-5
+    assert np.abs(prob.sum(-1) - 1).max() < 1e-5
+
+
+@pytest.mark.parametrize("name", MG.SAMPLE_NAMES)
+def test_inference_reference_sample_images(name):
+    """Real 960x540 frames through the drop-in CLI's preprocessing and the engine forward."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "..", "unet-image-segmentation_amd", "scripts"))
+    import inference
+    g = _load("samples.npz")
+    x, bgr, h, w = inference.load_and_preprocess_image(os.path.join(HERE, "samples", name + ".png"), 256, 256)
+    assert (h, w) == (960, 540) and x.shape == (1, 256, 256, 3)
+    assert abs(float(x.astype(np.float64).sum()) - float(g[name + ":x_sum"])) < 1e-6 * abs(float(g[name + ":x_sum"]))
+    assert np.array_equal(x[:, ::8, ::8, :], g[name + ":x_s8"])
+    m = _model(256, 1, g["w_seed"])
+    prob = inference.predict_mask(m, x)
+    assert prob.shape == (256, 256, 1)
+    _check_binary(prob[None], g[name + ":prob"], "sample:" + name)
+
+
+def _flips(engine, cache, p):
+    """ReLU decisions (and 2x2 max-pool argmax decisions) on which the device forward and the
+    float64 oracle differ: each sits within fp32 rounding of its decision boundary."""
+    A = engine._acts_last
+    relu, pool = 0, 0
+    for b in engine.blocks:
+        bb = A.blocks[b.name]
+        pre_h = (bb.z.cpu().double() * bb.scale.cpu().double() + bb.shift.cpu().double()).numpy()
+        rec = cache[b.name]
+        inv = p[f"{b.name}_bn/gamma"] / np.sqrt(rec["var"] + 1e-3)
+        pre_o = rec["z"] * inv + (p[f"{b.name}_bn/beta"] - rec["mean"] * inv)
+        relu += int(((pre_h > 0) != (pre_o > 0)).sum())
+        if b.name.startswith("enc") and b.name.endswith("block2"):
+            args = []
+            for pre in (pre_h, pre_o):
+                N, H, W, C = pre.shape
+                a = np.maximum(pre, 0).reshape(N, H // 2, 2, W // 2, 2, C).transpose(0, 1, 3, 5, 2, 4).reshape(-1, 4)
+                args.append(np.where(a.max(1) > 0, a.argmax(1), -1))
+            pool += int((args[0] != args[1]).sum())
+    return relu, pool
+
+
+def test_train_step_128_batch4():
+    from unet_amd.model import UNetModel
+    from unet_amd.optim import AdamW
+    g = _load("train128.npz")
+    m = UNetModel((128, 128, 3), 1, dropout_rate=0.0)
+    w = MG.model_weights(1, MG.FULL, int(g["w_seed"]))
+    m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+    x = MG.U(int(g["x_seed"]), (4, 128, 128, 3))
+    y = MG.quad_masks(4, 128, 128)
+    m.compile(AdamW(2e-3, 1e-4), "dice_loss")
+    res = m.train_step(x.astype(np.float32), y.astype(np.float32)).cpu().numpy()
+    torch.cuda.synchronize()
+    grads = {k: host(t) for k, t in m.engine.gvars.items()}
+    neww = m.engine.get_weights_dict()
+    # the float64 oracle, live, for every gradient tensor
+    orc = UNetOracle(1, 0.0)
+    prob, cache, _ = orc.forward(w, x, training=True)
+    lval, dprob = orc.loss_and_dprob(y, prob)
+    gref, _ = orc.backward(w, cache, dprob)
+    relu_flips, pool_flips = _flips(m.engine, cache, w)
+    # fp32 conditioning: the same oracle step in float32 (its own distance to float64, flips included)
+    w32 = {k: v.astype(np.float32) for k, v in w.items()}
+    prob32, cache32, _ = orc.forward(w32, x.astype(np.float32), training=True)
+    _, dprob32 = orc.loss_and_dprob(y.astype(np.float32), prob32)
+    g32, _ = orc.backward(w32, cache32, dprob32)
+    errs = {k: norm_err(grads[k], gref[k]) for k in gref}
+    e32 = {k: norm_err(g32[k], gref[k]) for k in gref}
+    worst = sorted(((k, e, e32[k]) for k, e in errs.items()), key=lambda r: -r[1])[:5]
+    _log({"test": "train128", "loss": float(res[0]), "loss_ref": float(lval), "relu_flips": relu_flips,
+          "pool_flips": pool_flips, "max_grad_rel_l2": worst[0][1], "worst(name, hip, fp32-oracle)": worst,
+          "max_fp32_oracle_rel_l2": max(e32.values())})
+    assert abs(res[0] - g["loss"]) < 1e-5 and abs(res[1] - g["dice"]) < 1e-5
+    assert abs(lval - g["loss"]) < 1e-12
+    assert set(errs) == set(grads)
+    bad = {k: (e, e32[k]) for k, e in errs.items() if e > max(2e-3, 2.0 * e32[k])}
+    assert not bad, bad
+    for k, v in g.items():
+        if k.startswith("gnorm:"):
+            hn = float(np.linalg.norm(grads[k[6:]]))
+            assert abs(hn - v) <= 1e-2 * v + 1e-12, (k, hn, float(v))
+        elif k.startswith("new256:"):
+            name = k[7:]
+            got = neww[name].reshape(-1)[:256].astype(np.float64)
+            assert np.abs(got - v).max() <= 1e-4 * max(np.abs(v).max(), 1e-3), name
