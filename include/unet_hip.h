@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 4
+#define UNET_ABI_VERSION 5
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -317,12 +317,16 @@ int unet_dice_fwd(const float* y_true, const float* y_pred, int n,
                   unet_stream_t stream);
 /* Backward of (1 - mean dice) [or 1 - mean iou] through the head
  * activation and the 1x1 conv: dx (n,h,w,Cin) grad w.r.t. the head input
- * view; dkernel (1,1,Cin,ncls), dbias (ncls) overwrite.                    */
+ * view; dkernel (1,1,Cin,ncls), dbias (ncls) overwrite.  loss_scale (> 0)
+ * multiplies the loss gradient: 1 for the reference's single-process step;
+ * n_local * world / n_global for a data-parallel shard, so that the summed
+ * all-reduce times 1/world is the gradient of the global-batch mean.       */
 size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls);
 int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
                   const float* kernel, const float* prob,
                   const float* y_true, const float* sums, float smooth,
-                  int loss_kind, float* dx, float* dkernel, float* dbias,
+                  int loss_kind, float loss_scale, float* dx, float* dkernel,
+                  float* dbias,
                   void* ws, size_t ws_bytes, unet_stream_t stream);
 /* Binary head on a BNRELU view: unet_head_bwd plus the BatchNorm-backward
  * partial sums of the head input's block (dx is all of its da; bn_partials
@@ -331,7 +335,8 @@ int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncl
 int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls,
                           const float* kernel, const float* prob,
                           const float* y_true, const float* sums, float smooth,
-                          int loss_kind, float* dx, float* dkernel, float* dbias,
+                          int loss_kind, float loss_scale, float* dx,
+                          float* dkernel, float* dbias,
                           const float* mean, const float* rstd,
                           float* bn_partials, void* ws, size_t ws_bytes,
                           unet_stream_t stream);

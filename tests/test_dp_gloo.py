@@ -37,18 +37,23 @@ def _worker(rank, world, port, q):
         scale = b.finish()
         ref = torch.arange(n, dtype=torch.float32) * sum(range(1, world + 1))
         ok1 = torch.equal(g, ref) and abs(scale - 1.0 / world) < 1e-12
-        # oracle-as-compute DP: per-rank dice-loss gradient on its shard, averaged
+        # oracle-as-compute DP with UNEQUAL shards (5 images: 3+2 over 2 ranks, 2+1+1+1 over 4):
+        # each rank's gradient of its shard-mean dice loss, weighted n_local * world / n_global
+        # (the head backward's loss_scale), summed by the all-reduce and scaled 1/world (AdamW's
+        # grad_scale), must be the gradient of the global-batch mean loss
         from oracle import keras_ops as K
+        G = 5
         rng = np.random.default_rng(0)
-        yt = (rng.random((8, 8, 8, 1)) > 0.5).astype(np.float64)
-        yp = rng.random((8, 8, 8, 1))
-        lo, hi = shard_bounds(8, world, rank)
-        gl = torch.from_numpy(K.dice_loss_grad(yt[lo:hi], yp[lo:hi]).sum(axis=(1, 2, 3)))
-        full = torch.zeros(8, dtype=torch.float64)
+        yt = (rng.random((G, 8, 8, 1)) > 0.5).astype(np.float64)
+        yp = rng.random((G, 8, 8, 1))
+        lo, hi = shard_bounds(G, world, rank)
+        loss_scale = (hi - lo) * world / G
+        gl = torch.from_numpy(loss_scale * K.dice_loss_grad(yt[lo:hi], yp[lo:hi]))
+        full = torch.zeros((G, 8, 8, 1), dtype=torch.float64)
         full[lo:hi] = gl
         dist.all_reduce(full)
-        ref2 = K.dice_loss_grad(yt, yp).sum(axis=(1, 2, 3)) * world  # per-shard mean rescaled
-        ok2 = np.allclose(full.numpy() / world, ref2 / world)
+        ref2 = K.dice_loss_grad(yt, yp)
+        ok2 = np.allclose(full.numpy() / world, ref2, rtol=1e-12, atol=1e-15)
         q.put((rank, ok1, ok2))
     finally:
         dist.destroy_process_group()

@@ -1,8 +1,8 @@
 """Data-parallel train step on the GPU, two ranks (tools/dp_check.py under torch.distributed.run).
 On a one-GPU box both ranks share device 0 and gloo carries the collectives (RCCL refuses two
 ranks on one GPU); the engine's bucketed, hook-driven all-reduce and its deferred weight
-gradients are the same code the RCCL run uses.  Every rank must end the step with bitwise
-identical averaged gradients and weights."""
+gradients are the same code the RCCL run uses.  The step must equal the shard-weighted average
+of single-process steps, and every rank must end it with bitwise identical gradients and weights."""
 import os
 import socket
 import subprocess
@@ -23,8 +23,12 @@ def _free_port():
 
 
 @pytest.mark.gpu
-def test_dp_two_ranks_consistent():
+@pytest.mark.parametrize("global_batch", [4, 5])
+def test_dp_two_ranks_equal_weighted_single_process(global_batch):
+    """tools/dp_check.py: the DP step equals sum_r (n_r / n) x (single-process gradient of shard r)
+    through AdamW (equal shards 2+2 and unequal 3+2), and the ranks agree bitwise."""
     env = dict(os.environ)
+    env["DP_CHECK_GLOBAL"] = str(global_batch)
     if torch.cuda.device_count() < 2:
         env["UNET_DP_ONE_DEVICE"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -32,3 +36,4 @@ def test_dp_two_ranks_consistent():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "identical across ranks: True" in r.stdout
+    assert r.stdout.count("equal to expected: True") == 2, r.stdout[-2000:]

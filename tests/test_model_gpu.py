@@ -114,20 +114,16 @@ def test_builder_api_and_inference_parity_cfg1():
                                                         (1, False, 0.0, "dice_loss", "auto"),
                                                         (1, True, 0.0, "iou_loss", "auto"),
                                                         (1, True, 0.0, "dice_loss", "always"),
-                                                        (1, True, 0.2, "dice_loss", "always"),
-                                                        (1, True, 0.2, "dice_loss", "chunked"),
-                                                        (1, False, 0.0, "dice_loss", "chunked")])
+                                                        (1, True, 0.2, "dice_loss", "always")])
 def test_train_step_parity(ncls, use_bn, drop, loss, fuse, record_property):
     """One train step against the oracle; fuse="always" runs the fused depthwise+pointwise
-    forward on every level it supports (32x32 and 16x16 here), "never" the split kernels;
-    "chunked" runs the top level's backward GEMM / depthwise data gradient in 2 batch chunks."""
+    forward on every level it supports (32x32 and 16x16 here), "never" the split kernels."""
     from unet_amd.model import UNetModel
     from unet_amd.optim import AdamW
     n, hw = 2, 32
     model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
-    model.engine.fuse_sepconv = "auto" if fuse == "chunked" else fuse
+    model.engine.fuse_sepconv = fuse
     model.engine.fuse_bn_bwd = fuse != "never"  # "never": also the separate BN-backward dz pass
-    model.engine.l0_chunks = 2 if fuse == "chunked" else 1
     orc = UNetOracle(ncls, drop, use_bn)
     lr, wd = 2e-3, 1e-4
     okind = "dice" if loss == "dice_loss" else "iou"

@@ -369,6 +369,13 @@ def test_head_dice(ops, ncls, loss_kind):
     assert rel_err(host(dx), rdx) < 1e-4
     assert rel_err(host(dk), rdk) < 1e-4
     assert rel_err(host(db), rdb) < 1e-4
+    # loss_scale (data-parallel shard weight) scales every gradient linearly
+    ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, loss_kind, dx, dk, db, loss_scale=0.75)
+    assert rel_err(host(dx), 0.75 * rdx) < 1e-4
+    assert rel_err(host(dk), 0.75 * rdk) < 1e-4
+    assert rel_err(host(db), 0.75 * rdb) < 1e-4
+    with pytest.raises(Exception):
+        ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, loss_kind, dx, dk, db, loss_scale=0.0)
 
 
 @pytest.mark.parametrize("ncls,thr", [(2, None), (2, 0.5), (5, None), (3, 0.3)])

@@ -1,8 +1,18 @@
-"""Multi-rank consistency check of the data-parallel train step (run under torch.distributed.run;
-with UNET_DP_ONE_DEVICE=1 every rank shares GPU 0 and gloo carries the collectives).  Each rank
-trains on its own synthetic shard; after the bucketed all-reduce every rank must hold bitwise the
-same averaged gradients and the same post-AdamW weights (a bucket all-reduced before its
-gradients were final, or never, shows up as a rank-dependent difference)."""
+"""Data-parallel correctness check (run under torch.distributed.run; with UNET_DP_ONE_DEVICE=1
+every rank shares GPU 0 and gloo carries the collectives).
+
+Each rank trains one DP step on its shard of a global batch of DP_CHECK_GLOBAL synthetic images
+(default 5 over 2 ranks: shards of 3 and 2, so the per-shard loss weighting is exercised).
+Then every rank rebuilds the expected result WITHOUT data parallelism: for each shard r a fresh
+single-process model (same initial weights, same dropout stream as rank r) takes a step on that
+shard alone (per-replica BatchNorm, as in DP), giving the gradient g_r of the shard's mean loss;
+the global-batch gradient is sum_r (n_r / n_global) g_r, and AdamW applied to it gives the
+expected weights.  Checked:
+  * DP gradients == that weighted average (relative L2 <= 1e-6 per tensor);
+  * DP weights after AdamW == the expected weights (max |diff| <= 1e-6 relative);
+  * BN moving statistics after sync_bn_statistics == mean of the per-shard models' statistics;
+  * every rank holds bitwise identical gradients and weights.
+A bucket summed twice or never, a wrong 1/world scale or a wrong shard weight fails the check."""
 import os
 import sys
 
@@ -12,30 +22,71 @@ import torch
 import torch.distributed as dist
 
 from bench import synthetic_batch
-from unet_amd.dp import init_from_env
+from unet_amd.dp import init_from_env, shard_bounds
 from unet_amd.model import UNetModel
 from unet_amd.optim import AdamW
 
 rank, world, local = init_from_env()
 dev = torch.device("cuda", local)
 torch.cuda.set_device(dev)
-m = UNetModel((64, 64, 3), 1, dropout_rate=0.2, device=dev)
-m.compile(AdamW(2e-3, 1e-4), "dice_loss")
-m.enable_data_parallel(bucket_bytes=1 << 20)  # many buckets: exercises the held low-water mark
-x, y = synthetic_batch(4, 64, 64, 1, 77 + rank, dev)
-for _ in range(3):
-    m.train_step(x, y)
+G = int(os.environ.get("DP_CHECK_GLOBAL", "5"))
+HW, SEED, LR, WD = 64, 5, 2e-3, 1e-4
+x_all, y_all = synthetic_batch(G, HW, HW, 1, 77, dev)
+lo, hi = shard_bounds(G, world, rank)
+
+m = UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED)
+m.compile(AdamW(LR, WD), "dice_loss")
+m.enable_data_parallel(bucket_bytes=1 << 20)  # many buckets
+m.train_step(x_all[lo:hi], y_all[lo:hi], global_size=G)
 torch.cuda.synchronize()
-g = m.engine.grads.detach().clone().cpu()
-p = m.engine.params.detach().clone().cpu()
+m.sync_bn_statistics()
+g_dp = m.engine.grads.detach().clone()
+p_dp = m.engine.params.detach().clone()
+s_dp = m.engine.stats.detach().clone()
+
+# expected, single-process per shard
+exp_g = torch.zeros_like(g_dp, dtype=torch.float64)
+exp_s = torch.zeros_like(s_dp, dtype=torch.float64)
+for r in range(world):
+    a, b = shard_bounds(G, world, r)
+    ref = UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED)
+    ref.engine.rank_salt = r
+    ref.compile(AdamW(LR, WD), "dice_loss")
+    ref.train_step(x_all[a:b], y_all[a:b])
+    torch.cuda.synchronize()
+    exp_g += ref.engine.grads.double() * ((b - a) / G)
+    exp_s += ref.engine.stats.double() / world
+    del ref
+base = UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED)
+opt = AdamW(LR, WD)
+exp_g32 = exp_g.float()
+opt.apply(base.engine.params, exp_g32, 1.0)
+torch.cuda.synchronize()
+
+worst_g = 0.0
+for s in m.engine.specs:
+    if not s.trainable:
+        continue
+    o = m.engine.train_layout.offsets[s.name]
+    # the all-reduced buffer holds the SUM of the weighted shard gradients; AdamW applies 1/world
+    a, b = g_dp[o:o + s.size].double() / world, exp_g[o:o + s.size]
+    e = float((a - b).norm() / (b.norm() + 1e-30))
+    worst_g = max(worst_g, e)
+p_err = float((p_dp.double() - base.engine.params.double()).abs().max() / base.engine.params.double().abs().max())
+s_err = float((s_dp.double() - exp_s).abs().max() / (exp_s.abs().max() + 1e-30))
+ok_vals = worst_g <= 1e-6 and p_err <= 1e-6 and s_err <= 1e-6
+
+g = g_dp.cpu()
+p = p_dp.cpu()
 gs = [torch.empty_like(g) for _ in range(world)]
 ps = [torch.empty_like(p) for _ in range(world)]
 dist.all_gather(gs, g)
 dist.all_gather(ps, p)
-ok = all(torch.equal(gs[0], t) for t in gs) and all(torch.equal(ps[0], t) for t in ps)
-nz = float((g != 0).float().mean())
+ok_same = all(torch.equal(gs[0], t) for t in gs) and all(torch.equal(ps[0], t) for t in ps)
+print(f"dp_check rank {rank}/{world} shard [{lo},{hi}) of {G}: grad rel-L2 vs weighted single-process "
+      f"{worst_g:.2e}, params {p_err:.2e}, bn stats {s_err:.2e}; equal to expected: {ok_vals}", flush=True)
 if rank == 0:
-    print(f"dp_check world={world}: grads/params identical across ranks: {ok} (nonzero grad fraction {nz:.3f})")
+    print(f"dp_check world={world}: grads/params identical across ranks: {ok_same}", flush=True)
 dist.barrier()
 dist.destroy_process_group()
-sys.exit(0 if ok else 1)
+sys.exit(0 if (ok_same and ok_vals) else 1)

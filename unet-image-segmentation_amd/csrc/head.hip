@@ -567,9 +567,9 @@ int head_bwd_grid(int64_t M) {
     return (int)(g > 1024 ? 1024 : g);
 }
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
-                  const float* y_true, const float* sums, float smooth, int loss_kind, float* dx, float* dkernel,
-                  float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs, float* bnpart,
-                  unet_stream_t stream);
+                  const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
+                  float* dkernel, float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs,
+                  float* bnpart, unet_stream_t stream);
 }  // namespace
 
 extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls) {
@@ -580,31 +580,33 @@ extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int
 
 extern "C" int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
                                      const float* prob, const float* y_true, const float* sums, float smooth,
-                                     int loss_kind, float* dx, float* dkernel, float* dbias, const float* mean,
+                                     int loss_kind, float loss_scale, float* dx, float* dkernel, float* dbias,
+                                     const float* mean,
                                      const float* rstd, float* bn_partials, void* ws, size_t ws_bytes,
                                      unet_stream_t stream) {
     UNET_CHECK_ARG(unet_head_bwd_bnstats_slabs(x, n, h, w, ncls) > 0,
                    "unet_head_bwd_bnstats: needs a binary head on a BNRELU view with Cin %% 4 == 0");
     UNET_CHECK_ARG(bn_partials, "unet_head_bwd_bnstats: null bn_partials");
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_head_bwd_bnstats: mean and rstd go together");
-    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, dx, dkernel, dbias, ws,
-                         ws_bytes, mean, rstd, bn_partials, stream);
+    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, loss_scale, dx, dkernel,
+                         dbias, ws, ws_bytes, mean, rstd, bn_partials, stream);
 }
 
 extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
                              const float* prob, const float* y_true, const float* sums, float smooth, int loss_kind,
-                             float* dx, float* dkernel, float* dbias, void* ws, size_t ws_bytes,
+                             float loss_scale, float* dx, float* dkernel, float* dbias, void* ws, size_t ws_bytes,
                              unet_stream_t stream) {
-    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, dx, dkernel, dbias, ws,
-                         ws_bytes, nullptr, nullptr, nullptr, stream);
+    return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, loss_scale, dx, dkernel,
+                         dbias, ws, ws_bytes, nullptr, nullptr, nullptr, stream);
 }
 
 namespace {
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
-                  const float* y_true, const float* sums, float smooth, int loss_kind, float* dx, float* dkernel,
-                  float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs, float* bnpart,
-                  unet_stream_t stream) {
+                  const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
+                  float* dkernel, float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs,
+                  float* bnpart, unet_stream_t stream) {
     if (check_view(x, "unet_head_bwd", true)) return -1;
+    UNET_CHECK_ARG(loss_scale > 0.0f && loss_scale < 1e30f, "unet_head_bwd: loss_scale must be finite and > 0");
     UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
                    "unet_head_bwd: input view must be PLAIN or BNRELU");
     UNET_CHECK_ARG(x->c0 <= kMaxCin, "unet_head_bwd: Cin %d > %d", x->c0, kMaxCin);
@@ -616,7 +618,9 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
     const int64_t M = (int64_t)n * h * w;
     const int64_t hw = (int64_t)h * w;
     hipStream_t st = as_stream(stream);
-    const float gscale = 1.0f / (float)((int64_t)n * ncls);
+    // d(mean over the n*ncls (image, class) terms)/dp, times the caller's loss scale (data
+    // parallelism with unequal shards: n_local * world / n_global, 1 otherwise)
+    const float gscale = loss_scale / (float)((int64_t)n * ncls);
     const DView v = make_dview(*x);
     const int CQ = x->c0 / 4;
     if (ncls == 1 && 256 % CQ == 0) {

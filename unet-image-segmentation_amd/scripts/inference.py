@@ -5,11 +5,12 @@ Same positional/optional flags and defaults (reference scripts/inference.py:54-9
 validation and exit codes (:207-215, :228-239), same preprocessing quirk: the image is fed as
 BGR (cv2.imread order, :100-110) although training used RGB; resized bilinear to 256x256 and
 scaled by 1/255; the probability map is resized back bilinear, thresholded (> threshold ->
-255) and saved; the largest connected region's bounding box crops the original image.
-OpenCV is not available in this image: PIL does the I/O and resizes with cv2's
-INTER_LINEAR formula (half-pixel centres, no antialias); the largest external contour is
-approximated by the largest 8-connected foreground component (scipy.ndimage).  This
-post-processing is off the GPU path.
+255) and saved; the bounding box of the external contour of largest cv2.contourArea crops
+the original image.  OpenCV is not available in this image: PIL does the I/O, and
+unet_amd/imageproc.py restates cv2.resize INTER_LINEAR (half-pixel centres, no antialias) and
+findContours(RETR_EXTERNAL) + contourArea (shoelace area of the traced boundary-pixel chain,
+holes included) + boundingRect.  The reference's own sample output (samples/usage) pins the
+crop (tests/test_imageproc.py).  This post-processing is off the GPU path.
 """
 import argparse
 import os
@@ -19,6 +20,8 @@ PROJECT_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 sys.path.append(PROJECT_ROOT)
 
 import numpy as np  # noqa: E402
+
+from unet_amd.imageproc import largest_external_contour, resize_linear  # noqa: E402
 
 IMG_HEIGHT = 256
 IMG_WIDTH = 256
@@ -39,30 +42,6 @@ def parse_args(argv=None) -> argparse.Namespace:
     parser.add_argument("--min_area", type=float, default=MIN_CONTOUR_AREA,
                         help=f"Minimum contour area threshold for cropping (default: {MIN_CONTOUR_AREA}).")
     return parser.parse_args(argv)
-
-
-def resize_linear(img: np.ndarray, out_h: int, out_w: int) -> np.ndarray:
-    """cv2.resize(..., INTER_LINEAR) for float images: half-pixel centres, edge clamp."""
-    h, w = img.shape[:2]
-
-    def coords(n_out, n_in):
-        s = (np.arange(n_out) + 0.5) * (n_in / n_out) - 0.5
-        s = np.clip(s, 0, n_in - 1)
-        i0 = np.floor(s).astype(np.int64)
-        i1 = np.minimum(i0 + 1, n_in - 1)
-        return i0, i1, (s - i0).astype(np.float32)
-
-    y0, y1, fy = coords(out_h, h)
-    x0, x1, fx = coords(out_w, w)
-    a = img[y0][:, x0]
-    b = img[y0][:, x1]
-    c = img[y1][:, x0]
-    d = img[y1][:, x1]
-    fx = fx[None, :, None] if img.ndim == 3 else fx[None, :]
-    fy = fy[:, None, None] if img.ndim == 3 else fy[:, None]
-    top = a + (b - a) * fx
-    bot = c + (d - c) * fx
-    return (top + (bot - top) * fy).astype(np.float32)
 
 
 def load_and_preprocess_image(input_path, target_height, target_width):
@@ -93,7 +72,6 @@ def predict_mask(model, input_tensor):
 
 def postprocess_and_save_results(prob, original_bgr, orig_h, orig_w, out_mask, out_crop, thr=0.5, min_area=100.0):
     from PIL import Image
-    from scipy import ndimage
     print("Processing predicted mask...")
     resized = resize_linear(prob[..., 0], orig_h, orig_w)
     binary = (resized > thr).astype(np.uint8) * 255
@@ -102,18 +80,14 @@ def postprocess_and_save_results(prob, original_bgr, orig_h, orig_w, out_mask, o
         os.makedirs(os.path.dirname(out_mask), exist_ok=True)
     Image.fromarray(binary).save(out_mask)
     print("Finding largest contour for cropping...")
-    lab, n = ndimage.label(binary > 0, structure=np.ones((3, 3)))
-    if n == 0:
+    best = largest_external_contour(binary)
+    if best is None:
         print("No contours found in the binary mask. Cropped image not saved.")
         return
-    areas = ndimage.sum(np.ones_like(lab), lab, index=np.arange(1, n + 1))
-    k = int(np.argmax(areas)) + 1
-    area = float(areas[k - 1])
-    if area <= min_area:
+    area, (x, y, w, h) = best
+    if not area > min_area:
         print(f"Largest contour area ({area:.0f}) is below minimum threshold ({min_area:.0f}). Cropped image not saved.")
         return
-    ys, xs = np.nonzero(lab == k)
-    y, x, h, w = ys.min(), xs.min(), ys.max() - ys.min() + 1, xs.max() - xs.min() + 1
     print(f"Largest contour area: {area:.0f} > {min_area:.0f}. Cropping region: (x={x}, y={y}, w={w}, h={h})")
     crop = original_bgr[y:y + h, x:x + w][..., ::-1]
     print(f"Saving cropped image to {out_crop} ...")

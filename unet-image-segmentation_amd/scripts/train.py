@@ -83,6 +83,9 @@ def main(argv=None):
     say(f"Seed          : {SEED}")
     say(f"GPUs          : {world} (data parallel)")
     say("------------------------------\n")
+    if args.batch_size < world:  # every data-parallel rank needs at least one sample per step
+        print(f"Error: --batch-size {args.batch_size} is smaller than the {world} data-parallel ranks.")
+        sys.exit(1)
 
     say("Setting up Data Generators...")
     try:

@@ -5,8 +5,17 @@ shared by image and mask (the reference synchronises the two generators through 
 shuffling for training only.  Data-parallel: every rank walks the same global batch order and
 keeps its own shard of each global batch, so N ranks x (batch/N) == one global batch.
 
-Decoding runs on the host (PIL); batches are handed to the GPU as pinned tensors.  The exact
-Keras RNG stream is not reproduced (TF's generator is not portable).
+Decoding runs on the host (PIL) in a background thread pool, a few batches ahead of the step
+(`Prefetcher`), and each batch is copied into page-locked host memory and sent to the device
+with a non-blocking copy on a dedicated stream, so neither decoding nor the H2D copy sits on the
+train step's critical path.  The exact Keras RNG stream is not reproduced (TF's generator is
+not portable).
+
+Data-parallel sharding: with W ranks every global batch of B samples is cut into W shards
+(remainder to the low ranks; `dp.shard_bounds`).  A trailing global batch with fewer than W
+samples would leave some rank without a sample, so it is skipped on every rank alike.  Each
+yielded batch carries `global_size` (the samples of the whole global batch), from which the
+engine weights its shard's loss gradient (model.train_step).
 """
 from __future__ import annotations
 
@@ -16,6 +25,26 @@ from typing import Iterator, Tuple
 import numpy as np
 
 from .dp import shard_bounds
+
+
+class Shard(tuple):
+    """(images, masks) of this rank's shard; .global_size = samples in the whole global batch."""
+
+    global_size: int = 0
+
+    def __new__(cls, x, y, global_size):
+        t = super().__new__(cls, (x, y))
+        t.global_size = int(global_size)
+        return t
+
+
+def global_batches(samples: int, batch_size: int, world: int):
+    """[start, stop) of the global batches of one pass over `samples` (trailing batches with
+    fewer samples than ranks are dropped: every rank must get at least one)."""
+    for b0 in range(0, samples, batch_size):
+        b1 = min(b0 + batch_size, samples)
+        if b1 - b0 >= world:
+            yield b0, b1
 
 IMG_EXT = (".png", ".jpg", ".jpeg", ".bmp", ".tif", ".tiff", ".ppm")
 
@@ -37,7 +66,9 @@ def load_image(path, size, mode):
 
 class PairLoader:
     def __init__(self, frames_dir, masks_dir, size, batch_size, seed, shuffle=True, horizontal_flip=False, rank=0,
-                 world=1):
+                 world=1, workers=4):
+        if batch_size < world:
+            raise ValueError(f"batch size {batch_size} < {world} data-parallel ranks: every rank needs a sample")
         self.frames = [os.path.join(frames_dir, f) for f in _list(frames_dir)]
         self.masks = [os.path.join(masks_dir, f) for f in _list(masks_dir)]
         if len(self.frames) != len(self.masks):
@@ -45,6 +76,8 @@ class PairLoader:
         self.size, self.batch_size, self.seed = size, batch_size, seed
         self.shuffle, self.flip, self.rank, self.world = shuffle, horizontal_flip, rank, world
         self.samples = len(self.frames)
+        self.workers = max(1, int(workers))
+        self._pool = None
 
     def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
         epoch = 0
@@ -52,26 +85,39 @@ class PairLoader:
             rng = np.random.default_rng(self.seed + epoch)
             order = rng.permutation(self.samples) if self.shuffle else np.arange(self.samples)
             flips = rng.random(self.samples) < 0.5 if self.flip else np.zeros(self.samples, bool)
-            for b0 in range(0, self.samples, self.batch_size):
-                idx = order[b0:b0 + self.batch_size]
+            for b0, b1 in global_batches(self.samples, self.batch_size, self.world):
+                idx = order[b0:b1]
                 lo, hi = shard_bounds(len(idx), self.world, self.rank)
-                idx = idx[lo:hi]
-                xs, ys = [], []
-                for i in idx:
-                    x = load_image(self.frames[i], self.size, "rgb")
-                    y = load_image(self.masks[i], self.size, "grayscale")
-                    if flips[i]:
-                        x, y = x[:, ::-1], y[:, ::-1]
-                    xs.append(x)
-                    ys.append(y)
-                yield np.ascontiguousarray(np.stack(xs)), np.ascontiguousarray(np.stack(ys))
+                yield Shard(*self.load(idx[lo:hi], flips), global_size=len(idx))
             epoch += 1
+
+    def _sample(self, i, flip):
+        x = load_image(self.frames[i], self.size, "rgb")
+        y = load_image(self.masks[i], self.size, "grayscale")
+        if flip:
+            x, y = x[:, ::-1], y[:, ::-1]
+        return x, y
+
+    def load(self, idx, flips):
+        """Decode the samples idx (PIL releases the GIL while decoding / resizing, so a small
+        thread pool decodes a batch in parallel); returns contiguous (x, y) batches."""
+        if self.workers > 1 and len(idx) > 1:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(self.workers, thread_name_prefix="unet-decode")
+            pairs = list(self._pool.map(lambda i: self._sample(int(i), bool(flips[i])), idx))
+        else:
+            pairs = [self._sample(int(i), bool(flips[i])) for i in idx]
+        return (np.ascontiguousarray(np.stack([p[0] for p in pairs])),
+                np.ascontiguousarray(np.stack([p[1] for p in pairs])))
 
 
 class synthetic_pairs:
     """N synthetic (image, mask) pairs: U[0,1) images, ID-card-like quad masks (~30% fg)."""
 
     def __init__(self, n, size, batch_size, seed, shuffle=True, rank=0, world=1):
+        if batch_size < world:
+            raise ValueError(f"batch size {batch_size} < {world} data-parallel ranks: every rank needs a sample")
         self.samples, self.size, self.batch_size, self.seed = n, size, batch_size, seed
         self.shuffle, self.rank, self.world = shuffle, rank, world
 
@@ -91,9 +137,9 @@ class synthetic_pairs:
         while True:
             rng = np.random.default_rng(self.seed + epoch)
             order = rng.permutation(self.samples) if self.shuffle else np.arange(self.samples)
-            for b0 in range(0, self.samples, self.batch_size):
-                idx = order[b0:b0 + self.batch_size]
+            for b0, b1 in global_batches(self.samples, self.batch_size, self.world):
+                idx = order[b0:b1]
                 lo, hi = shard_bounds(len(idx), self.world, self.rank)
                 pairs = [self._pair(int(i)) for i in idx[lo:hi]]
-                yield np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])
+                yield Shard(np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs]), global_size=len(idx))
             epoch += 1

@@ -9,8 +9,13 @@ memory growth).  Design for MI355X:
     buffer to its start; the engine reports a low-water offset after every layer and a
     bucket is all-reduced (async, on RCCL's stream) as soon as it is complete, so the
     collectives overlap the remaining backward kernels;
-  * the average (x 1/world) is folded into the AdamW kernel's grad_scale: no extra pass;
-  * BatchNorm statistics are per replica (the tf.distribute default, synchronized=False).
+  * the average (x 1/world) is folded into the AdamW kernel's grad_scale: no extra pass; a
+    rank whose shard is not 1/world of the global batch weights its loss gradient by
+    n_local * world / n_global (head backward's loss_scale), so the result is the gradient of
+    the global-batch mean for any split;
+  * BatchNorm batch statistics are per replica (the tf.distribute default, synchronized=False);
+    the moving statistics are averaged over ranks before validation / checkpoints
+    (model.sync_bn_statistics; tf.distribute reads them as a MEAN over replicas).
 """
 from __future__ import annotations
 
@@ -50,6 +55,16 @@ def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
     if not dist.is_initialized():
         dist.init_process_group(backend=backend)
     return rank, world, local
+
+
+def average_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place mean of a tensor over the ranks (sum all-reduce, then x 1/world)."""
+    if dist.is_initialized():
+        world = dist.get_world_size(group)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            t.mul_(1.0 / world)
+    return t
 
 
 class GradBucketer:

@@ -71,6 +71,7 @@ class BlockBufs:
     coef: Optional[torch.Tensor] = None  # BN-backward coefficients (mean, dbeta/M, rstd*dgamma/M)
     bnpart: Optional[torch.Tensor] = None  # BN-backward partial sums emitted by the producer of da
     bn_slabs: int = 0  # > 0: bnpart holds this many fresh slabs for the next backward of the block
+    bnpart_s: int = -1  # the slab count bnpart's counters were last laid out for
 
 
 @dataclass
@@ -127,16 +128,14 @@ class UNetEngine:
         self._build_plan()
         self._acts: Dict[int, Acts] = {}
         self.step_count = 0
+        self.rank_salt = 0  # data-parallel rank (dropout streams); set by model.enable_data_parallel
         self.grad_hook: Optional[Callable[[int], None]] = None  # called with a flat-offset low-water mark
-        # Off-critical-path backward work (weight gradients of the pointwise and depthwise
-        # convolutions) runs on a second HIP stream, overlapping the data-gradient chain.
-        # The critical path runs on a high-priority stream (model.train_step enters it) so the
-        # dispatcher hands freed CU slots to its workgroups before the side stream's; the side
-        # stream's weight-gradient grids otherwise hold slots the data-gradient chain waits for.
+        # Off-critical-path backward work (weight gradients of the pointwise, depthwise and
+        # transposed convolutions) runs on a second HIP stream, overlapping the data-gradient
+        # chain on the main stream.
         lo_prio, hi_prio = torch.cuda.Stream.priority_range()
-        prio = os.environ.get("UNET_PRIO", "1") != "0"
-        self.main = torch.cuda.Stream(device=self.device, priority=hi_prio if prio else 0)
-        self.side = torch.cuda.Stream(device=self.device, priority=lo_prio if prio else 0)
+        self.main = torch.cuda.Stream(device=self.device, priority=hi_prio)
+        self.side = torch.cuda.Stream(device=self.device, priority=lo_prio)
         self.overlap = os.environ.get("UNET_OVERLAP", "1") != "0"  # 0: single stream (clean profiles)
         # Fused depthwise+pointwise forward (unet_sepconv_fwd) vs the two launches: "auto" uses it
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
@@ -145,41 +144,13 @@ class UNetEngine:
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
         # BN-backward statistics of a block emitted by the launch that completes its da (the next
-        # block's depthwise data gradient through BN+ReLU or the max-pool), not by a pass over (da, z)
-        self.fuse_bn_stats = os.environ.get("UNET_FUSE_BN_STATS", "1") != "0"
-        # the pointwise weight gradient forms dz from (da, z) itself, so the data-gradient GEMM on the
-        # critical path does not store dz (its HBM write moves to a read on the side stream).  Off:
-        # measured 3 % slower (1231 vs 1269 img/s, r1w) -- the two streams share HBM, so moving bytes
-        # between them does not shorten the step; only removing bytes does.
-        self.wgrad_forms_dz = os.environ.get("UNET_WGRAD_DZ", "0") != "0"
-        # depthwise data + filter gradient in one pass over dy (unet_dwconv3x3_bwd) on the main stream.
-        # Off: it saves one dy read but moves the filter work onto the critical path; measured
-        # 1245 vs 1258 img/s (r1x)
-        self.fuse_dw_bwd = os.environ.get("UNET_FUSE_DW_BWD", "0") != "0"
-        # 256x256 level: run the data-gradient GEMM and the depthwise data gradient in batch chunks,
-        # interleaved, so each chunk's dy is consumed while it is still in the Infinity Cache
-        self.l0_chunks = int(os.environ.get("UNET_L0_CHUNKS", "1"))
-        # decoder levels whose weight gradients are deferred until the backward reaches the
-        # bottleneck: they are HBM-bound and then overlap the MFMA-bound deep levels instead of
-        # contending with the HBM-bound 256x256 / 128x128 data-gradient chain (measured 1272 ->
-        # 1296 img/s, r1za).  With all-reduce hooks the low-water mark is held back until the
-        # deferred work is issued, so buckets still complete from the end of the flat buffer.
-        dl = os.environ.get("UNET_DEFER_WGRAD", "")
-        self.defer_wgrad_levels = {int(t) for t in dl.split(",") if t.strip()}
-        # Conv2DTranspose weight / bias gradients on the side stream (its data gradient stays on
-        # the critical path); the side stream is otherwise idle until the deferred work is issued
-        self.convt_wgrad_side = os.environ.get("UNET_CONVT_SIDE", "1") != "0"
-        # Conv2DTranspose data gradient emits the BN-backward partials of the block below (no pass over da, z)
-        self.convt_bn_stats = os.environ.get("UNET_CONVT_BNSTATS", "1") != "0"
-        # cross-stream waits through device-scope events (no system-scope fence per marker)
-        self.device_events = os.environ.get("UNET_DEVICE_EVENTS", "1") != "0"
-        self.last_wgrad_main = os.environ.get("UNET_LAST_WGRAD_MAIN", "1") != "0"
+        # block's depthwise data gradient through BN+ReLU or the max-pool, the Conv2DTranspose data
+        # gradient, the head), not by a separate pass over (da, z)
+        self.fuse_bn_stats = True
         # image block (4 padded channels): data and pointwise weight gradient in one streaming pass over
         # (da, z, y) that forms dz on the fly, so dz (M x 64) is neither stored nor re-read
-        self.img_fused_wgrad = os.environ.get("UNET_IMG_WGRAD", "1") != "0"
+        self.img_fused_wgrad = True
         self._ev = None  # created on first use (on the device)
-        self._deferred: List = []
-        self._held_mark: Optional[int] = None
 
     # ------------------------------------------------------------------ weights ------
     def set_weights_dict(self, weights: Dict[str, np.ndarray]) -> None:
@@ -342,6 +313,10 @@ class UNetEngine:
         return xp
 
     def drop_seeds(self, step: int) -> Dict[str, int]:
+        """Dropout seeds of a step, per site; data-parallel ranks salt them with their rank so the
+        replicas draw independent masks (rank_salt 0 = the single-process stream)."""
+        if self.rank_salt:
+            return {s: _mix64(self.seed, step, i + 1, self.rank_salt) for i, s in enumerate(DROP_SITES)}
         return {s: _mix64(self.seed, step, i + 1) for i, s in enumerate(DROP_SITES)}
 
     def forward(self, x: torch.Tensor, training: bool = False, seeds: Optional[Dict[str, int]] = None) -> torch.Tensor:
@@ -390,7 +365,7 @@ class UNetEngine:
 
     # ----------------------------------------------------------------- backward ------
     def _event(self):
-        if self._ev is None and self.device_events:
+        if self._ev is None:
             self._ev = ops.DeviceEvent()
         return self._ev
 
@@ -413,9 +388,6 @@ class UNetEngine:
         the hook (bucketed all-reduce) is issued from the side stream after it has caught up
         with the main stream."""
         if self.grad_hook is not None:
-            if self._deferred:  # gradients above this mark are not all issued yet: hold the mark
-                self._held_mark = self.train_layout.offsets[name]
-                return
             if self.overlap:
                 self._side_wait_main()
                 with torch.cuda.stream(self.side):
@@ -423,11 +395,23 @@ class UNetEngine:
             else:
                 self.grad_hook(self.train_layout.offsets[name])
 
+    def _bnpart(self, tb: BlockBufs, S: int, c: int) -> torch.Tensor:
+        """tb's producer-side BN-backward partials buffer sized for S slabs.  Its arrival counters
+        sit at an S-dependent offset (lastblock.h), so a buffer last used with another S is
+        re-zeroed, not just reused."""
+        need = ops.bn_stats_partials_numel(S, c)
+        if tb.bnpart is None or tb.bnpart.numel() < need:
+            tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
+        elif tb.bnpart_s != S:
+            tb.bnpart.zero_()
+        tb.bnpart_s = S
+        return tb.bnpart[:need]
+
     def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0,
                    stats_target: Optional[BlockBufs] = None):
         """Backward of one conv_block.  stats_target: the block whose output view_in reads (through
-        BN+ReLU or the max-pool) when this launch completes its da (dx0); on the fused path the
-        depthwise data gradient then also emits that block's BN-backward partials."""
+        BN+ReLU or the max-pool) when this launch completes its da (dx0); the depthwise data
+        gradient then also emits that block's BN-backward partials."""
         n = A.n
         h, w = self._dims(b.level)
         m = n * h * w
@@ -442,151 +426,65 @@ class UNetEngine:
         else:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
         dk, pk = self._wts(b, refresh=False)
+        img_wg = False
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
             if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
-                ops.bn_relu_bwd_stats_finish(bb.bnpart, bb.bn_slabs, m, b.cout, bb.mean, bb.rstd, self.use_bn,
-                                             dgamma, dbeta, bb.coef)
+                ops.bn_relu_bwd_stats_finish(bb.bnpart[:ops.bn_stats_partials_numel(bb.bn_slabs, b.cout)],
+                                             bb.bn_slabs, m, b.cout, bb.mean, bb.rstd, self.use_bn, dgamma, dbeta,
+                                             bb.coef)
             else:
                 ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
-            wdz = self.wgrad_forms_dz and drop_rate == 0.0
-            img_wg = (self.img_fused_wgrad and not wdz and drop_rate == 0.0 and b.cin == 4
-                      and b.cout in (32, 64))
-            chunked = (self.l0_chunks > 1 and b.level == 0 and dx0 is not None and not wdz and drop_rate == 0.0
-                       and view_in.drop_rate == 0.0 and n % self.l0_chunks == 0 and not self.fuse_dw_bwd)
-            if chunked:  # chunk 0 only; the others are interleaved with the depthwise data gradient below
-                nc = n // self.l0_chunks
-                ops.pointwise_bwd_data_bnrelu(bb.da[:nc], bb.z[:nc], nc * h * w, b.cin, b.cout, pk, bb.scale,
-                                              bb.shift, bb.coef, 0.0, 0, dy.view(n, h, w, b.cin)[:nc],
-                                              dz.view(n, h, w, b.cout)[:nc])
-            elif img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
+            img_wg = self.img_fused_wgrad and drop_rate == 0.0 and b.cin == 4 and b.cout in (32, 64)
+            if img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
                 ops.pointwise_bwd_data_bnrelu_wgrad(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                                     bb.y, dy, self._gwts(b)[1])
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
-                                              drop_rate, drop_seed, dy, None if wdz else dz)
+                                              drop_rate, drop_seed, dy, dz)
         else:
-            wdz = chunked = img_wg = False
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gdk, gpk = self._gwts(b)
 
-        fused_dw = (self.fuse_dw_bwd and dx0 is not None and not b.wcin
-                    and ops.dwconv3x3_bwd_slabs(view_in, n, h, w) > 0)
-
         def weight_grads():
-            if img_wg:
-                pass  # already accumulated by the data-gradient GEMM
-            elif wdz:
-                ops.pointwise_bwd_filter_bnrelu(bb.y, bb.da, bb.z, m, b.cin, b.cout, bb.scale, bb.shift, bb.coef, gpk)
-            else:
+            if not img_wg:  # (the image block's was accumulated by its data-gradient pass)
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            if not fused_dw:
-                ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
                 self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
 
-        defer = (self.overlap and b.name.startswith("dec")
-                 and b.level in self.defer_wgrad_levels and not chunked)
-        if defer:  # issued on the side stream later (_flush_deferred), after this point of main
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-            self._deferred.append((ev, weight_grads))
-        elif not chunked:  # (chunked: after all chunks' data gradients, below)
-            # the image block (dx0 None) has no data gradient after this: its weight gradients run
-            # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
-            if self.overlap and not (dx0 is None and self.last_wgrad_main):
-                self._side_wait_main()
-                with torch.cuda.stream(self.side):
-                    weight_grads()
-            else:
+        # the image block (dx0 None) has no data gradient after this: its weight gradients run
+        # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
+        if self.overlap and dx0 is not None:
+            self._side_wait_main()
+            with torch.cuda.stream(self.side):
                 weight_grads()
-        if chunked:
-            K = self.l0_chunks
-            nc, mc = n // K, (n // K) * h * w
-            dy4, dz4 = dy.view(n, h, w, b.cin), dz.view(n, h, w, b.cout)
-            tb = stats_target if (stats_target is not None and self.fuse_bn_stats) else None
-            Sc = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in.batch(slice(0, nc)), nc, h, w) if tb is not None else 0
-            if Sc > 0:
-                need = ops.bn_stats_partials_numel(K * Sc, view_in.channels)
-                if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
-            for c in range(K):
-                sl = slice(c * nc, (c + 1) * nc)
-                if c > 0:  # chunk 0's data gradient was issued before the side-stream fork
-                    ops.pointwise_bwd_data_bnrelu(bb.da[sl], bb.z[sl], mc, b.cin, b.cout, pk, bb.scale, bb.shift,
-                                                  bb.coef, 0.0, 0, dy4[sl], dz4[sl])
-                sub = view_in.batch(sl)
-                if Sc > 0:
-                    ops.dwconv3x3_bwd_data_bnstats(sub, nc, h, w, dk, dy4[sl], dx0[sl],
-                                                   tb.mean if self.use_bn else None,
-                                                   tb.rstd if self.use_bn else None,
-                                                   tb.bnpart[c * Sc * 2 * view_in.channels:][:ops.bn_stats_partials_numel(Sc, view_in.channels)])
-                else:
-                    ops.dwconv3x3_bwd_data(sub, nc, h, w, dk, dy4[sl], dx0[sl], dx1[sl] if dx1 is not None else None)
-            if Sc > 0:
-                tb.bn_slabs = K * Sc
-            if self.overlap:
-                self._side_wait_main()
-                with torch.cuda.stream(self.side):
-                    weight_grads()
-            else:
-                weight_grads()
-        elif fused_dw:
-            S = ops.dwconv3x3_bwd_slabs(view_in, n, h, w)
-            tb = stats_target if (stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd) else None
-            if tb is not None:
-                need = ops.bn_stats_partials_numel(S, view_in.channels)
-                if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
-                ops.dwconv3x3_bwd(view_in, n, h, w, dk, dy, dx0, dx1, gdk, tb.mean if self.use_bn else None,
-                                  tb.rstd if self.use_bn else None, tb.bnpart)
-                tb.bn_slabs = S
-            else:
-                ops.dwconv3x3_bwd(view_in, n, h, w, dk, dy, dx0, dx1, gdk)
-        elif dx0 is not None:
+        else:
+            weight_grads()
+        if dx0 is not None:
             S = 0
             if stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
                 S = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w)
             if S > 0:
                 tb = stats_target
-                need = ops.bn_stats_partials_numel(S, view_in.channels)
-                if tb.bnpart is None or tb.bnpart.numel() < need:
-                    tb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
                 ops.dwconv3x3_bwd_data_bnstats(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
-                                               tb.rstd if self.use_bn else None, tb.bnpart)
+                                               tb.rstd if self.use_bn else None, self._bnpart(tb, S, view_in.channels))
                 tb.bn_slabs = S
             else:
                 ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
-    def _flush_deferred(self, count: Optional[int] = None):
-        """Issue deferred weight-gradient work on the side stream: all of it, or `count` closures
-        (a few per block, so the host keeps the critical path's queue fed meanwhile)."""
-        k = len(self._deferred) if count is None else min(count, len(self._deferred))
-        for ev, fn in self._deferred[:k]:
-            self.side.wait_event(ev)
-            with torch.cuda.stream(self.side):
-                fn()
-        self._deferred = self._deferred[k:]
-        if self._deferred:
-            return
-        if self._held_mark is not None and self.grad_hook is not None:
-            self._side_wait_main()
-            with torch.cuda.stream(self.side):
-                self.grad_hook(self._held_mark)
-        self._held_mark = None
-
     def _view_of(self, A: Acts, b: Block) -> View:
         bb = A.blocks[b.name]
         return View.bnrelu(bb.z, bb.scale, bb.shift)
 
-    def backward(self, y_true: torch.Tensor, loss_kind: int = L.LOSS_DICE) -> None:
-        """Gradients of the loss of the last training forward into self.grads."""
+    def backward(self, y_true: torch.Tensor, loss_kind: int = L.LOSS_DICE, loss_scale: float = 1.0) -> None:
+        """Gradients of loss_scale x the loss of the last training forward into self.grads."""
         A = self._acts_last
         n = A.n
         seeds = self._last_seeds
@@ -596,18 +494,15 @@ class UNetEngine:
         S = (ops.head_bwd_bnstats_slabs(hv, n, self.h, self.w, self.num_classes)
              if self.fuse_bn_stats and self.fuse_bn_bwd else 0)
         if S > 0:  # the head's dx is all of the last block's da: emit its BN-backward partials too
-            need = ops.bn_stats_partials_numel(S, hv.channels)
-            if lb.bnpart is None or lb.bnpart.numel() < need:
-                lb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
             ops.head_bwd_bnstats(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"], A.prob,
                                  y_true, A.sums, SMOOTH, loss_kind, lb.da, self.gvars["output_mask/kernel"],
                                  self.gvars["output_mask/bias"], lb.mean if self.use_bn else None,
-                                 lb.rstd if self.use_bn else None, lb.bnpart)
+                                 lb.rstd if self.use_bn else None, self._bnpart(lb, S, hv.channels), loss_scale)
             lb.bn_slabs = S
         else:
             ops.head_bwd(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
                          A.prob, y_true, A.sums, SMOOTH, loss_kind, lb.da,
-                         self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"])
+                         self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"], loss_scale)
         self._grads_ready("output_mask/kernel")
         nd = len(self.dec)
         for i in reversed(range(nd)):
@@ -627,40 +522,27 @@ class UNetEngine:
             h, w = self._dims(b1.level + 1)
             gk, gb = self.gvars[f"{stage}_upsample/kernel"], self.gvars[f"{stage}_upsample/bias"]
             pb = A.blocks[prev.name]
+            uk = self.vars[f"{stage}_upsample/kernel"]
             S = 0
-            if self.convt_bn_stats and self.fuse_bn_stats and self.fuse_bn_bwd:
+            if self.fuse_bn_stats and self.fuse_bn_bwd:
                 S = ops.conv_transpose2x2_bwd_data_bnstats_slabs(xv, n, h, w, fi)
+            # data gradient on the critical path (emitting the BN partials of the block below when it
+            # can), weight + bias gradients on the side stream
             if S > 0:
-                need = ops.bn_stats_partials_numel(S, xv.c0)
-                if pb.bnpart is None or pb.bnpart.numel() < need:
-                    pb.bnpart = torch.zeros(need, dtype=torch.float32, device=self.device)
-                ops.conv_transpose2x2_bwd_data_bnstats(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
-                                                       A.dup[stage], pb.da, pb.mean if self.use_bn else None,
-                                                       pb.rstd if self.use_bn else None, pb.bnpart)
+                ops.conv_transpose2x2_bwd_data_bnstats(xv, n, h, w, fi, uk, A.dup[stage], pb.da,
+                                                       pb.mean if self.use_bn else None,
+                                                       pb.rstd if self.use_bn else None, self._bnpart(pb, S, xv.c0))
                 pb.bn_slabs = S
-                if self.overlap and self.convt_wgrad_side:
-                    self._side_wait_main()
-                    with torch.cuda.stream(self.side):
-                        ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
-                                                  A.dup[stage], None, gk, gb)
-                else:
-                    ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
-                                              None, gk, gb)
-            elif self.overlap and self.convt_wgrad_side:
-                # data gradient on the critical path, weight + bias gradients on the side stream
-                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
-                                          A.blocks[prev.name].da, None, None)
+            else:
+                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, uk, A.dup[stage], pb.da, None, None)
+            if self.overlap:
                 self._side_wait_main()
                 with torch.cuda.stream(self.side):
-                    ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
-                                              None, gk, gb)
+                    ops.conv_transpose2x2_bwd(xv, n, h, w, fi, uk, A.dup[stage], None, gk, gb)
             else:
-                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"], A.dup[stage],
-                                          A.blocks[prev.name].da, gk, gb)
+                ops.conv_transpose2x2_bwd(xv, n, h, w, fi, uk, A.dup[stage], None, gk, gb)
             self._grads_ready(f"{stage}_upsample/kernel")
         b1, b2 = self.bneck
-        self._flush_deferred()  # deferred decoder weight gradients overlap the deep levels (all at once:
-        # issuing them a few per block measured slower, 1278 vs 1301 img/s)
         self._block_bwd(A, b2, self._view_of(A, b1), A.blocks[b1.name].da,
                         drop_rate=self.dropout_rate if drop else 0.0,
                         drop_seed=seeds["bneck_dropout"] if drop else 0, stats_target=A.blocks[b1.name])
@@ -675,7 +557,6 @@ class UNetEngine:
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
-        self._flush_deferred()
         if self.overlap:
             self._main_wait_side()
 

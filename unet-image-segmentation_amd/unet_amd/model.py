@@ -72,16 +72,30 @@ class UNetModel:
 
     def enable_data_parallel(self, bucket_bytes: int = 6 << 20, group=None):
         """Average gradients over torch.distributed ranks each step (bucketed, overlapped)."""
+        import torch.distributed as dist
         self.bucketer = GradBucketer(self.engine.grads, bucket_bytes, group)
         self.engine.grad_hook = self.bucketer.ready
+        self.engine.rank_salt = dist.get_rank(group) if dist.is_initialized() else 0
 
-    def train_step(self, x, y) -> torch.Tensor:
-        """One optimisation step; returns the device vector [loss, dice_coef, iou_coef]
-        (asynchronous: nothing here waits for the GPU)."""
+    def train_step(self, x, y, global_size: Optional[int] = None) -> torch.Tensor:
+        """One optimisation step; returns the device vector [loss, dice_coef, iou_coef] of this
+        rank's batch (asynchronous: nothing here waits for the GPU).
+
+        Data parallel: x is this rank's shard of a global batch of `global_size` samples (default:
+        equal shards).  The shard's loss gradient is weighted n_local * world / global_size and
+        the all-reduced sum scaled by 1/world, which is the gradient of the global-batch mean
+        loss for any split (utils/loss.py:25-29 means over (image, class) terms)."""
         if self.optimizer is None:
             self.compile()
         x = as_device_tensor(x, self.engine.device)
         y = as_device_tensor(y, self.engine.device)
+        loss_scale = 1.0
+        if self.bucketer is not None and self.bucketer.world > 1:
+            n_local, world = x.shape[0], self.bucketer.world
+            n_global = int(global_size) if global_size else n_local * world
+            if n_global < world or n_local < 1:
+                raise ValueError(f"shard of {n_local} from a global batch of {n_global} over {world} ranks")
+            loss_scale = n_local * world / n_global
         caller = torch.cuda.current_stream(self.engine.device)
         main = self.engine.main
         main.wait_stream(caller)
@@ -92,7 +106,7 @@ class UNetModel:
             if self.loss_kind == L.LOSS_IOU:
                 res = res.clone()
                 res[0] = 1.0 - res[2]
-            self.engine.backward(y, self.loss_kind)
+            self.engine.backward(y, self.loss_kind, loss_scale)
             scale = self.bucketer.finish() if self.bucketer is not None else 1.0
             self.optimizer.apply(self.engine.params, self.engine.grads, scale)
         caller.wait_stream(main)
@@ -145,7 +159,7 @@ class UNetModel:
         cbs = CallbackList(callbacks or [], self)
         hist = History()
         self.stop_training = False
-        it = iter(x)
+        it = iter(self._prefetch(x))
         cbs.on_train_begin()
         for epoch in range(epochs):
             cbs.on_epoch_begin(epoch)
@@ -155,14 +169,15 @@ class UNetModel:
             nsteps = 0
             t0 = time.time()
             for step in range(steps_per_epoch or 1):
-                xb, yb = next(it)
-                res = self.train_step(xb, yb)
+                batch = next(it)
+                res = self.train_step(batch[0], batch[1], getattr(batch, "global_size", None))
                 acc = res.detach().clone() if acc is None else acc + res
                 nsteps += 1
             logs = self._log_values(acc / nsteps)
             if self.mean_iou is not None:
                 self.mean_iou.all_reduce()
                 logs[self.mean_iou.name] = self.mean_iou.result()
+            self.sync_bn_statistics()
             if validation_data is not None:
                 logs.update(self.evaluate(validation_data, steps=validation_steps, prefix="val_"))
             for k, v in logs.items():
@@ -176,19 +191,39 @@ class UNetModel:
             if self.stop_training:
                 break
         cbs.on_train_end()
+        if hasattr(it, "close"):
+            it.close()
         return hist
 
+    def _prefetch(self, data):
+        """Wrap a host-batch iterable in the background decoder / async H2D prefetcher."""
+        from .prefetch import Prefetcher
+        if isinstance(data, Prefetcher) or not hasattr(data, "__iter__"):
+            return data
+        return Prefetcher(data, self.engine.device)
+
+    def sync_bn_statistics(self):
+        """Data parallel: average the BatchNorm moving statistics over the ranks (tf.distribute
+        keeps them sync-on-read MEAN; the moving update is linear, so averaging at any point
+        leaves the mean's trajectory unchanged).  Called before validation and so before every
+        checkpoint; a no-op on one process."""
+        from .dp import average_
+        if self.bucketer is not None and self.bucketer.world > 1:
+            average_(self.engine.stats, self.bucketer.group)
+
     def evaluate(self, data, steps: Optional[int] = None, prefix: str = "") -> Dict[str, float]:
-        it = iter(data)
+        it = iter(self._prefetch(data))
         if self.mean_iou is not None:
             saved = self.mean_iou.confusion.clone()
             self.mean_iou.reset_state()
         acc, n = None, 0
         for _ in range(steps or 1):
-            xb, yb = next(it)
-            res = self.test_step(xb, yb)
+            batch = next(it)
+            res = self.test_step(batch[0], batch[1])
             acc = res.detach().clone() if acc is None else acc + res
             n += 1
+        if hasattr(it, "close"):
+            it.close()
         logs = self._log_values(acc / n, prefix)
         if self.mean_iou is not None:
             self.mean_iou.all_reduce()

@@ -520,7 +520,7 @@ def dice_fwd(y_true: Tensor, y_pred: Tensor, n: int, hw: int, ncls: int, smooth:
 
 
 def head_bwd(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, sums: Tensor, smooth: float,
-             loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor):
+             loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor, loss_scale: float = 1.0):
     _check(prob, "prob", n * h * w * ncls)
     _check(y_true, "y_true", n * h * w * ncls)
     _check(dx, "dx", n * h * w * x.c0)
@@ -529,7 +529,7 @@ def head_bwd(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, su
     m = n * h * w
     _call("unet_head_bwd", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
           ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums),
-           float(smooth), int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), ws, wsb, _stream())
+          float(smooth), int(loss_kind), float(loss_scale), _ptr(dx), _ptr(dk), _ptr(db), ws, wsb, _stream())
 
 
 def head_bwd_bnstats_slabs(x: View, n, h, w, ncls) -> int:
@@ -538,7 +538,8 @@ def head_bwd_bnstats_slabs(x: View, n, h, w, ncls) -> int:
 
 
 def head_bwd_bnstats(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, sums: Tensor, smooth: float,
-                     loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor, mean, rstd, partials: Tensor):
+                     loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor, mean, rstd, partials: Tensor,
+                     loss_scale: float = 1.0):
     """head_bwd that also emits the BN-backward partials of the head input's block."""
     S = head_bwd_bnstats_slabs(x, n, h, w, ncls)
     _check(prob, "prob", n * h * w * ncls)
@@ -550,7 +551,8 @@ def head_bwd_bnstats(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Te
     m = n * h * w
     _call("unet_head_bwd_bnstats", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
           ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums), float(smooth),
-          int(loss_kind), _ptr(dx), _ptr(dk), _ptr(db), _ptr(mean), _ptr(rstd), _ptr(partials), ws, wsb, _stream())
+          int(loss_kind), float(loss_scale), _ptr(dx), _ptr(dk), _ptr(db), _ptr(mean), _ptr(rstd), _ptr(partials), ws,
+          wsb, _stream())
 
 
 def meaniou_update(y_true: Tensor, y_pred: Tensor, num_classes: int, threshold: Optional[float],
