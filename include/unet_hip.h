@@ -174,6 +174,14 @@ int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int w, int cout
 int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                      int cout, const float* pw_kernel, float* y, float* z,
                      float* bn_partials, unet_stream_t stream);
+/* Kernel schedule of unet_sepconv_fwd (process-wide; returns the previous value, < 0 on a bad
+ * value).  AUTO: the register-A kernel (each lane computes the depthwise output straight in the
+ * MFMA operand layout) for BN+ReLU / concat / plain views of >= 64 channels, the LDS-A-tile
+ * kernel otherwise.  TILE / RK force one (RK fails with -1 where it does not exist): both are
+ * parity-tested (tests/test_ops_gpu.py).  Identical results: both form each output as the
+ * same k-ordered fmaf chain.                                                                  */
+enum { UNET_SEPCONV_AUTO = 0, UNET_SEPCONV_TILE = 1, UNET_SEPCONV_RK = 2 };
+int unet_sepconv_set_schedule(int schedule);
 
 /* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
  * momentum 0.99, epsilon 1e-3, biased batch variance for both the output

@@ -429,12 +429,25 @@ SEP_CASES = [
     (3, 2, 8, 32, 32, 32, 64, 0.0),
     (3, 1, 16, 16, 16, 16, 256, 0.2),
     (1, 1, 8, 16, 8, 0, 8, 0.0),     # K tail (8 channels < 16-channel stage)
+    # register-A kernel shapes (>= 64 channels): N tail (192 = 128 + 64), channel-stage tails, concat
+    (1, 2, 8, 32, 96, 0, 192, 0.0),
+    (3, 1, 16, 16, 64, 68, 64, 0.2),
+    (0, 1, 8, 16, 68, 0, 100, 0.0),
+    (1, 1, 16, 32, 256, 0, 256, 0.0),
 ]
+
+
+@pytest.fixture(params=["auto", "tile"])
+def sep_schedule(request, ops):
+    old = ops.sepconv_set_schedule(ops.SEPCONV_AUTO if request.param == "auto" else ops.SEPCONV_TILE)
+    yield request.param
+    ops.sepconv_set_schedule(old)
 
 
 @pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", SEP_CASES)
 @pytest.mark.parametrize("train", [True, False])
-def test_fused_sepconv(ops, mode, n, h, w, c0, c1, cout, drop, train):
+def test_fused_sepconv(ops, sep_schedule, mode, n, h, w, c0, c1, cout, drop, train):
+    """Both kernel schedules (auto: register-A where it exists; tile: the LDS-A-tile kernel)."""
     rng = np.random.default_rng(100 + mode + cout)
     a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
     C = c0 + c1
@@ -461,6 +474,47 @@ def test_fused_sepconv(ops, mode, n, h, w, c0, c1, cout, drop, train):
         assert rel_err(host(outs[1]), 1 / np.sqrt(var + 1e-3)) < 1e-5
     else:
         assert float(y.min()) == -7.0 and float(y.max()) == -7.0  # inference leaves y untouched
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", [c for c in SEP_CASES if c[0] != 2 and c[4] + c[5] >= 64])
+def test_sepconv_schedules_bitwise_equal(ops, mode, n, h, w, c0, c1, cout, drop):
+    """The register-A and LDS-A-tile kernels form every output as the same k-ordered fmaf chain:
+    z and y are bitwise equal; the per-tile BN partials (mean, M2) sum the tile's rows in a
+    different order (4 waves of 32 rows vs 2 of 64), so they agree to fp32 rounding."""
+    rng = np.random.default_rng(7 + cout)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk, pk = dev(rng.standard_normal((3, 3, C, 1))), dev(rng.standard_normal((1, 1, C, cout)) / np.sqrt(C))
+    v = _mk_view(ops, mode, t, drop, 5)
+    m = n * h * w
+    outs = []
+    for sch in (ops.SEPCONV_RK, ops.SEPCONV_TILE):
+        old = ops.sepconv_set_schedule(sch)
+        try:
+            y = torch.empty((n, h, w, C), device="cuda")
+            z = torch.empty((n, h, w, cout), device="cuda")
+            part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
+            ops.sepconv_fwd(v, n, h, w, dk, cout, pk, y, z, part)
+            torch.cuda.synchronize()
+            outs.append((y.cpu(), z.cpu(), part.cpu()))
+        finally:
+            ops.sepconv_set_schedule(old)
+    (y1, z1, p1), (y2, z2, p2) = outs
+    assert torch.equal(z1, z2) and torch.equal(y1, y2)
+    nb = (m + 127) // 128 * cout * 2
+    assert rel_err(p1[:nb].double().numpy(), p2[:nb].double().numpy()) < 1e-6
+
+
+def test_sepconv_schedule_rk_refuses_pool(ops):
+    x = torch.zeros((1, 16, 32, 64), device="cuda")
+    sc, sh = torch.ones(64, device="cuda"), torch.zeros(64, device="cuda")
+    old = ops.sepconv_set_schedule(ops.SEPCONV_RK)
+    try:
+        with pytest.raises(Exception):
+            ops.sepconv_fwd(ops.View.pool_bnrelu(x, sc, sh), 1, 8, 16, torch.zeros(9 * 64, device="cuda"), 64,
+                            torch.zeros(64 * 64, device="cuda"), None, torch.empty((1, 8, 16, 64), device="cuda"))
+    finally:
+        ops.sepconv_set_schedule(old)
 
 
 def test_fused_sepconv_unsupported_shapes(ops):

@@ -26,6 +26,7 @@ import numpy as np
 import pytest
 
 from helpers import host, norm_err
+from oracle import keras_ops as K
 from oracle.unet_ref import UNetOracle
 
 pytestmark = pytest.mark.gpu
@@ -177,6 +178,20 @@ def test_train_step_128_batch4():
             hn = float(np.linalg.norm(grads[k[6:]]))
             assert abs(hn - v) <= 1e-2 * v + 1e-12, (k, hn, float(v))
         elif k.startswith("new256:"):
+            # Keras AdamW's first step moves a weight by lr * g / (|g| + 3.2e-6): where |g| is
+            # within a few 1e-6 of 0 the step is set by the gradient's rounding, so compare
+            # there against AdamW applied to the device's own gradient (AdamW itself is tested
+            # exactly in test_ops_gpu); elsewhere against the float64 oracle's step (golden)
             name = k[7:]
             got = neww[name].reshape(-1)[:256].astype(np.float64)
-            assert np.abs(got - v).max() <= 1e-4 * max(np.abs(v).max(), 1e-3), name
+            if name not in gref:  # moving statistics
+                assert np.abs(got - v).max() <= 1e-4 * max(np.abs(v).max(), 1e-3), name
+                continue
+            gr = gref[name].reshape(-1)[:256]
+            sure = np.abs(gr) > 1e-4
+            tol = 1e-4 * max(np.abs(v).max(), 1e-3)
+            assert np.abs(got - v)[sure].max(initial=0.0) <= tol, name
+            w0 = w[name].reshape(-1)[:256]
+            gd = grads[name].reshape(-1)[:256]
+            own, _, _ = K.adamw_update(w0, gd, np.zeros_like(w0), np.zeros_like(w0), 1, 2e-3, 1e-4)
+            assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name

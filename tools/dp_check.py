@@ -8,8 +8,8 @@ single-process model (same initial weights, same dropout stream as rank r) takes
 shard alone (per-replica BatchNorm, as in DP), giving the gradient g_r of the shard's mean loss;
 the global-batch gradient is sum_r (n_r / n_global) g_r, and AdamW applied to it gives the
 expected weights.  Checked:
-  * DP gradients == that weighted average (relative L2 <= 1e-6 per tensor);
-  * DP weights after AdamW == the expected weights (max |diff| <= 1e-6 relative);
+  * DP gradients == that weighted average (relative L2 <= 1e-5 per tensor; fp32 rounding);
+  * DP weights after AdamW == the expected weights (max |diff| <= 1e-5 relative);
   * BN moving statistics after sync_bn_statistics == mean of the per-shard models' statistics;
   * every rank holds bitwise identical gradients and weights.
 A bucket summed twice or never, a wrong 1/world scale or a wrong shard weight fails the check."""
@@ -74,7 +74,10 @@ for s in m.engine.specs:
     worst_g = max(worst_g, e)
 p_err = float((p_dp.double() - base.engine.params.double()).abs().max() / base.engine.params.double().abs().max())
 s_err = float((s_dp.double() - exp_s).abs().max() / (exp_s.abs().max() + 1e-30))
-ok_vals = worst_g <= 1e-6 and p_err <= 1e-6 and s_err <= 1e-6
+# fp32 rounding only: the shard weight enters the DP backward at the loss (x n_r*world/n) and the
+# expected value after it; measured <= 1e-6 (2+2 shards) / 2.3e-6 (3+2 shards).  A bucket summed
+# twice or never, or a wrong scale, is an O(1e-1..1) error.
+ok_vals = worst_g <= 1e-5 and p_err <= 1e-5 and s_err <= 1e-6
 
 g = g_dp.cpu()
 p = p_dp.cpu()

@@ -1,0 +1,31 @@
+// Shared definitions of the fused SeparableConv2D forward kernels (sepconv.hip: the LDS-A-tile
+// schedule; sepconv_rk.hip: the register-A schedule).  Reference model/u_net.py:14-23.
+#pragma once
+#include "view.h"
+
+namespace unet {
+namespace sep {
+
+constexpr int TH = 8, TW = 16;            // pixel rectangle of one M tile
+constexpr int HHp = TH + 2, HWp = TW + 2; // halo
+constexpr int BK = 16;                    // channels per k-stage
+enum { E_STORE = 0, E_STATS = 1 };
+
+__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+struct SepArgs {
+    DView x;
+    int N, H, W, Cin, Cout;
+    const float* dk;  // (3,3,Cin,1)
+    const float* pk;  // (1,1,Cin,Cout): B(k, n) = pk[k*Cout + n] (n-contiguous)
+    float* y;         // optional (N,H,W,Cin)
+    float* z;         // (N,H,W,Cout)
+    float2* stats;    // [M/128][Cout]
+};
+
+// register-A schedule (sepconv_rk.hip): returns 0, or -1 if the mode/shape has no such kernel
+int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);
+bool rk_supported(int mode, int cin, int cout);
+
+}  // namespace sep
+}  // namespace unet

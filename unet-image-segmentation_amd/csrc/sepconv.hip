@@ -9,30 +9,14 @@
 // ds_read_b128 fragments as in gemm_rows_vec), then runs v_mfma_f32_32x32x2_f32 on it.
 // In training the first N-tile block also stores y (the depthwise output), which the pointwise
 // weight gradient needs; inference skips it.  Requires H % 8 == 0, W % 16 == 0, Cin % 4 == 0.
-#include "view.h"
+#include "sepconv.h"
 
 namespace unet {
 
 namespace {
-
-constexpr int TH = 8, TW = 16;            // pixel rectangle of one M tile
-constexpr int HHp = TH + 2, HWp = TW + 2; // halo
-constexpr int BK = 16;                    // channels per k-stage
+using namespace sep;
 constexpr int LR = BK + 4;                // LDS row stride (floats) of the A tile (conflict-free fragments)
 constexpr int XLR = BK;                   // halo pixel stride: lane-linear, conflict-free b128 reads
-enum { E_STORE = 0, E_STATS = 1 };
-
-__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
-
-struct SepArgs {
-    DView x;
-    int N, H, W, Cin, Cout;
-    const float* dk;  // (3,3,Cin,1)
-    const float* pk;  // (1,1,Cin,Cout): B(k, n) = pk[k*Cout + n] (n-contiguous)
-    float* y;         // optional (N,H,W,Cin)
-    float* z;         // (N,H,W,Cout)
-    float2* stats;    // [M/128][Cout]
-};
 
 // WN = waves along N (2 or 4); the block has 2 x WN waves, each owning a 64 x (BN / WN) piece of
 // the 128 x BN output tile.  Wide tiles (BN = 256, 8 waves) give two waves per SIMD, so one wave's
@@ -388,6 +372,17 @@ int launch(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
 
 using namespace unet;
 
+namespace {
+int g_sep_schedule = UNET_SEPCONV_AUTO;
+}
+
+extern "C" int unet_sepconv_set_schedule(int schedule) {
+    UNET_CHECK_ARG(schedule >= UNET_SEPCONV_AUTO && schedule <= UNET_SEPCONV_RK, "unet_sepconv_set_schedule: bad value");
+    const int old = g_sep_schedule;
+    g_sep_schedule = schedule;
+    return old;
+}
+
 extern "C" int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int w, int cout) {
     if (!x || n <= 0 || h <= 0 || w <= 0 || cout <= 0) return 0;
     const int C = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
@@ -419,6 +414,15 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     a.stats = reinterpret_cast<float2*>(bn_partials);
     const bool stats = bn_partials != nullptr, wy = y != nullptr, drop = x->drop_rate > 0.f;
     hipStream_t st = as_stream(stream);
+    // register-A schedule where it exists (BN+ReLU / concat / plain views, >= 64 channels) unless
+    // the LDS-A-tile schedule is forced; max-pool views keep the LDS-A-tile kernel (4 raw loads
+    // per halo element need its wider 8-wave staging)
+    if (g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout)) {
+        if (launch_rk(a, x->mode, drop, stats, wy, st)) return -1;
+        UNET_CHECK_LAUNCH("unet_sepconv_fwd");
+        return 0;
+    }
+    UNET_CHECK_ARG(g_sep_schedule != UNET_SEPCONV_RK, "unet_sepconv_fwd: no register-A kernel for this view / shape");
     switch (x->mode) {
         case UNET_VIEW_PLAIN:
             return drop ? launch<UNET_VIEW_PLAIN, true>(a, stats, wy, st) : launch<UNET_VIEW_PLAIN, false>(a, stats, wy, st);

@@ -337,6 +337,17 @@ def pointwise_bwd_filter_bnrelu(y: Tensor, da: Tensor, z: Tensor, m: int, cin: i
           _stream())
 
 
+SEPCONV_AUTO, SEPCONV_TILE, SEPCONV_RK = 0, 1, 2
+
+
+def sepconv_set_schedule(schedule: int) -> int:
+    """Kernel schedule of sepconv_fwd (see unet_sepconv_set_schedule); returns the previous one."""
+    r = L.load().unet_sepconv_set_schedule(int(schedule))
+    if r < 0:
+        raise ValueError(f"bad sepconv schedule {schedule}")
+    return r
+
+
 def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
     vs = x.c_struct()
     return bool(L.load().unet_sepconv_fwd_supported(ctypes.byref(vs), n, h, w, cout))
