@@ -80,10 +80,13 @@ int main(int argc, char** argv) {
     }
     shape<UNET_VIEW_BNRELU, 64, 2>("enc1_block2", N, 256, 256, 64, 64);
 
+    shape<UNET_VIEW_POOL_BNRELU, 128, 2>("enc2_block1", N, 128, 128, 64, 128);
     shape<UNET_VIEW_BNRELU, 128, 2>("enc2_block2", N, 128, 128, 128, 128);
+    shape<UNET_VIEW_POOL_BNRELU, 256, 4>("enc3_block1", N, 64, 64, 128, 256);
 
     shape<UNET_VIEW_BNRELU, 256, 4>("enc3_block2", N, 64, 64, 256, 256);
 
+    shape<UNET_VIEW_POOL_BNRELU, 256, 4>("enc4_block1", N, 32, 32, 256, 512);
     shape<UNET_VIEW_BNRELU, 256, 4>("enc4_block2", N, 32, 32, 512, 512);
     shape<UNET_VIEW_BNRELU, 256, 4>("dec3_block2", 16, 64, 64, 256, 256);
     shape<UNET_VIEW_BNRELU, 128, 2>("dec2_block2", 16, 128, 128, 128, 128);
