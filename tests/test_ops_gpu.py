@@ -434,6 +434,10 @@ SEP_CASES = [
     (3, 1, 16, 16, 64, 68, 64, 0.2),
     (0, 1, 8, 16, 68, 0, 100, 0.0),
     (1, 1, 16, 32, 256, 0, 256, 0.0),
+    # max-pool views on the register-A kernel; a grid with several tiles per persistent block
+    (2, 2, 8, 16, 64, 0, 128, 0.2),
+    (2, 1, 16, 32, 128, 0, 64, 0.0),
+    (1, 4, 128, 128, 64, 0, 192, 0.0),
 ]
 
 
@@ -476,7 +480,7 @@ def test_fused_sepconv(ops, sep_schedule, mode, n, h, w, c0, c1, cout, drop, tra
         assert float(y.min()) == -7.0 and float(y.max()) == -7.0  # inference leaves y untouched
 
 
-@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", [c for c in SEP_CASES if c[0] != 2 and c[4] + c[5] >= 64])
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", [c for c in SEP_CASES if c[4] + c[5] >= 64])
 def test_sepconv_schedules_bitwise_equal(ops, mode, n, h, w, c0, c1, cout, drop):
     """The register-A and LDS-A-tile kernels form every output as the same k-ordered fmaf chain:
     z and y are bitwise equal; the per-tile BN partials (mean, M2) sum the tile's rows in a
@@ -505,14 +509,14 @@ def test_sepconv_schedules_bitwise_equal(ops, mode, n, h, w, c0, c1, cout, drop)
     assert rel_err(p1[:nb].double().numpy(), p2[:nb].double().numpy()) < 1e-6
 
 
-def test_sepconv_schedule_rk_refuses_pool(ops):
-    x = torch.zeros((1, 16, 32, 64), device="cuda")
-    sc, sh = torch.ones(64, device="cuda"), torch.zeros(64, device="cuda")
+def test_sepconv_schedule_rk_refuses_narrow(ops):
+    """The register-A kernel needs >= 64 input and output channels; forcing it elsewhere errors."""
+    x = torch.zeros((1, 8, 16, 4), device="cuda")
     old = ops.sepconv_set_schedule(ops.SEPCONV_RK)
     try:
         with pytest.raises(Exception):
-            ops.sepconv_fwd(ops.View.pool_bnrelu(x, sc, sh), 1, 8, 16, torch.zeros(9 * 64, device="cuda"), 64,
-                            torch.zeros(64 * 64, device="cuda"), None, torch.empty((1, 8, 16, 64), device="cuda"))
+            ops.sepconv_fwd(ops.View.plain(x), 1, 8, 16, torch.zeros(9 * 4, device="cuda"), 64,
+                            torch.zeros(4 * 64, device="cuda"), None, torch.empty((1, 8, 16, 64), device="cuda"))
     finally:
         ops.sepconv_set_schedule(old)
 

@@ -10,21 +10,38 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // Register-A schedule.  The MFMA A operand (the depthwise output) is computed by each lane in
 // registers, straight in v_mfma_f32_32x32x2_f32's operand layout, from the staged halo: lane l of
-// wave w owns GEMM row w*32 + (l & 31), i.e. pixel (2w + ((l & 31) >> 4), l & 15) of the 8 x 16
-// tile, and for k-group g of a stage (8 channels) the 4 channels 8g + 4(l >> 5) + s, s = 0..3, so
+// wave w owns GEMM row w*32 + (l & 31), i.e. pixel (2w + (lo >> 4), rk_col(lo)) of the 8 x 16
+// tile (lo = l & 31; the second pixel row is rotated by two columns so that every 16-lane group of
+// a ds_read_b128 halo tap covers the 64 banks once: rows are 18 halo pixels apart, and without the
+// rotation two lanes of each group share a bank), and for k-group g of a stage (8 channels) the 4
+// channels 8g + 4(l >> 5) + s, s = 0..3, so
 // one ds_read_b128 of the halo per tap gives the 4 k-slots of 4 consecutive MFMA steps (the
 // k-slot permutation of gemm_rows_vec: MFMA step s takes channels 8g + s and 8g + 4 + s).
 // Each wave owns 32 rows x all BN columns, so every depthwise value is computed once per block
 // and no A tile goes through LDS: there is no depthwise -> MFMA hand-off inside a stage, only the
 // halo / B staging ring (three slots, ONE barrier per 16-channel stage).  The depthwise of the
 // next k-group (36 FMAs, 18 LDS reads) is interleaved with the MFMAs of the current one.
-//   LDS: halo [3][10*18 px][20] (16 channels + 4 pad: conflict-free b128 taps), taps [3][9][16],
+//   LDS (one buffer; the epilogue reuses it): halo [3][10*18 px][20] (16 channels + 4 pad), taps [3][9][16],
 //        B k-major [3][16][BN+4] (n contiguous: the staging stores are conflict-free float4s; the
 //        fragment of a tile and k-group is 4 conflict-free ds_read_b32 down a column).  An n-major
 //        image would give one b128 per fragment but its transposed staging stores are 16-way bank
 //        conflicted (measured: that alone cost more than the whole MFMA work of the kernel).
+//   Epilogue: each wave writes its 32 x BN accumulator tile into LDS and reads it back as row
+//   float4s, so z leaves as 16-byte stores of BN contiguous channels per pixel (the accumulator
+//   layout holds one column per lane: 4-byte stores, 2 rows x 128 B per instruction).
 constexpr int RX = BK + 4;                 // halo pixel stride (floats)
 constexpr int HPIX = HHp * HWp;            // 180 halo pixels
+
+// tile column of the pixel that lane lo (0..31) of a wave owns (row 2w + (lo >> 4))
+__device__ __forceinline__ int rk_col(int lo) { return lo < 16 ? lo : ((lo + 14) & 15); }
+template <int BN>
+struct RkLds {
+    static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = BK * (BN + 4);
+    static constexpr int RING = 3 * (XSZ + KSZ + BSZ);
+    static constexpr int TLD = BN + 4;                 // epilogue transpose row stride
+    static constexpr int EPI = 4 * 32 * TLD + 4 * BN;  // 4 waves' tiles + the statistics combine
+    static constexpr int SIZE = RING > EPI ? RING : EPI;
+};
 
 template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y>
 __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
@@ -34,9 +51,11 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     constexpr int NP = MODE == UNET_VIEW_POOL_BNRELU ? 4 : 1;
     constexpr int BQ = BN * (BK / 4) / 256;     // B float4 per thread per stage
     constexpr int LB = BN + 4;                  // k-major B row stride
-    __shared__ __attribute__((aligned(16))) float Xs[3][HPIX * RX];
-    __shared__ __attribute__((aligned(16))) float Ks[3][9 * BK];
-    __shared__ __attribute__((aligned(16))) float Bs[3][BK * LB];
+    using L = RkLds<BN>;
+    __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
+    auto Xs = [&](int b) { return smem + b * L::XSZ; };
+    auto Ks = [&](int b) { return smem + 3 * L::XSZ + b * L::KSZ; };
+    auto Bs = [&](int b) { return smem + 3 * (L::XSZ + L::KSZ) + b * L::BSZ; };
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
@@ -129,11 +148,11 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
                 v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
             }
             if (lp[j] < 0 || !cok) v = f4(0.f);
-            if (e < NH) *reinterpret_cast<float4*>(&Xs[buf][(e >> 2) * RX + 4 * (e & 3)]) = v;
+            if (e < NH) *reinterpret_cast<float4*>(&Xs(buf)[(e >> 2) * RX + 4 * (e & 3)]) = v;
         }
         if (tid < 9 * (BK / 4)) {
             const int c2 = hc - 4 * hq + 4 * (tid % (BK / 4));
-            *reinterpret_cast<float4*>(&Ks[buf][4 * tid]) = c2 < Cin ? htap : f4(0.f);
+            *reinterpret_cast<float4*>(&Ks(buf)[4 * tid]) = c2 < Cin ? htap : f4(0.f);
         }
     };
     // ---- B staging: thread loads float4 (k-row, n-quad) of the n-contiguous weights
@@ -152,11 +171,11 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     auto store_b = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r)
-            *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
+            *reinterpret_cast<float4*>(&Bs(buf)[(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
     };
 
-    // ---- this lane's pixel: tile row 2 wave + (lo >> 4), column lo & 15
-    const int pr = 2 * wave + (lo >> 4), pc = lo & 15;
+    // ---- this lane's pixel: tile row 2 wave + (lo >> 4), column rk_col(lo)
+    const int pr = 2 * wave + (lo >> 4), pc = rk_col(lo);
     const int xoff = (pr * HWp + pc) * RX + 4 * hi;  // halo tap (0, 0) of k-group 0
     float* yrow = nullptr;
     if constexpr (WRITE_Y) yrow = g.y + ((int64_t)(n * g.H + h0 + pr) * g.W + w0 + pc) * Cin + 4 * hi;
@@ -169,8 +188,8 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
 
     // depthwise output of k-group kg (this lane's pixel, 4 channels) from halo / tap buffer b
     auto dw = [&](int b, int kg) {
-        const float* X = Xs[b];
-        const float* Kt = Ks[b];
+        const float* X = Xs(b);
+        const float* Kt = Ks(b);
         float4 a = f4(0.f);
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
@@ -186,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     // NEXT k-group (buffer nb, group nkg): interleaved one MFMA : two LDS reads : two VALU ops, so
     // the depthwise runs in the MFMA pipe's shadow instead of between MFMA bursts
     auto mfma_dw = [&](const float4 a, int b, int kg, int nb, int nkg) {
-        const float* Bb = Bs[b];
+        const float* Bb = Bs(b);
         float4 bf[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
@@ -251,23 +270,18 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
         __syncthreads();
     }
 
-    // ---- epilogue: row p of the tile = pixel (h0 + p / 16, w0 + p % 16); this wave's rows are
-    // wave * 32 + acc_row(r, hi)
-    const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
+    // ---- epilogue (the loop ended on a barrier: the ring is free).  Accumulator row
+    // acc_row(r, hi) of wave w is tile pixel (2w + (row >> 4), rk_col(row)).
+    constexpr int TLD = L::TLD;
+    float* T = smem + wave * 32 * TLD;
+    float* red = smem + 4 * 32 * TLD;
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-        const int col = n0 + tn * 32 + lo;
-        if (col >= g.Cout) continue;
+    for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int p = wave * 32 + acc_row(r, hi);
-            g.z[(mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * g.Cout + col] = acc[tn][r];
-        }
-    }
+        for (int r = 0; r < 16; ++r) T[acc_row(r, hi) * TLD + tn * 32 + lo] = acc[tn][r];
     if constexpr (EPI == E_STATS) {
         // per column (mean, M2) of the tile's 128 rows: per-wave sums, a fixed-order combine of
-        // the 4 waves through LDS (the loop ended on a barrier, so Bs is free)
-        float* red = &Bs[0][0];
+        // the 4 waves through LDS
         float mean[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
@@ -306,6 +320,17 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
                         make_float2(mean[tn], (red[cl] + red[BN + cl]) + (red[2 * BN + cl] + red[3 * BN + cl]));
             }
         }
+    } else {
+        __syncthreads();
+    }
+    // z: the wave's 32 pixels x BN channels as float4s (BN / 4 per pixel, 64 per instruction)
+    constexpr int Q4 = BN / 4, NS = 32 * Q4 / 64;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int idx = i * 64 + lane, row = idx / Q4, q = idx - row * Q4;
+        const float4 v = *reinterpret_cast<const float4*>(&T[row * TLD + 4 * q]);
+        const int ph = h0 + 2 * wave + (row >> 4), pw = w0 + rk_col(row);
+        if (n0 + 4 * q < g.Cout) st4(g.z + ((int64_t)(n * g.H + ph) * g.W + pw) * g.Cout + n0 + 4 * q, v);
     }
 }
 
@@ -324,7 +349,11 @@ void launch_rk_t(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
 }  // namespace
 
 bool rk_supported(int mode, int cin, int cout) {
-    return mode != UNET_VIEW_POOL_BNRELU && cin >= 64 && cout >= 64;
+    // max-pool views only up to 128 output channels: wider layers keep the LDS-A-tile kernel's
+    // 256-wide 8-wave tile, which pools each halo element once for all columns (measured:
+    // tools/lab/sep_rk_lab.hip, enc3_block1 / enc4_block1)
+    return mode >= UNET_VIEW_PLAIN && mode <= UNET_VIEW_CONCAT && cin >= 64 && cout >= 64 &&
+           (mode != UNET_VIEW_POOL_BNRELU || cout <= 128);
 }
 
 int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st) {
@@ -338,6 +367,9 @@ int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, h
     switch (mode) {
         case UNET_VIEW_PLAIN: if (drop) UNET_RK(UNET_VIEW_PLAIN, true); else UNET_RK(UNET_VIEW_PLAIN, false); break;
         case UNET_VIEW_BNRELU: if (drop) UNET_RK(UNET_VIEW_BNRELU, true); else UNET_RK(UNET_VIEW_BNRELU, false); break;
+        case UNET_VIEW_POOL_BNRELU:
+            if (drop) UNET_RK(UNET_VIEW_POOL_BNRELU, true); else UNET_RK(UNET_VIEW_POOL_BNRELU, false);
+            break;
         default: if (drop) UNET_RK(UNET_VIEW_CONCAT, true); else UNET_RK(UNET_VIEW_CONCAT, false); break;
     }
 #undef UNET_RK
