@@ -128,8 +128,8 @@ __device__ __forceinline__ Moments moments_combine(Moments a, Moments b) {
 // ------------------------------------------------------------- host side ----
 // Deterministic ordered reduction of S slabs of L floats: out[l] = sum_s part[s*L + l]
 // (double accumulation, fixed order).  out has row stride ld_out for rows of `row`
-// floats (row == L, ld_out == L for a flat copy).
-int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out,
-                 hipStream_t stream);
+// floats (row == L, ld_out == L for a flat copy).  part is scratch: long, narrow reductions
+// sum chunks of slabs in place first (two fixed-order levels).
+int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream);
 
 }  // namespace unet

@@ -15,7 +15,7 @@ __device__ __forceinline__ void store_out(float* out, int64_t l, int64_t row, in
 
 // out[l] = sum_s part[s][l] with s in increasing order, in double.  Wide reductions (many
 // outputs): one thread per 4 consecutive outputs walks all S slabs with float4 loads.
-__global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restrict__ part, int S, int64_t L,
+__global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restrict__ part, int S, int64_t L, int64_t sp,
                                                            float* __restrict__ out, int64_t row, int64_t ld_out) {
     const int64_t l = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (l >= L) return;
@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restri
     for (; s + 4 <= S; s += 4) {
         float4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ld4(p + (int64_t)(s + u) * L);
+        for (int u = 0; u < 4; ++u) v[u] = ld4(p + (int64_t)(s + u) * sp);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             a0 += (double)v[u].x;
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restri
         }
     }
     for (; s < S; ++s) {
-        const float4 v = ld4(p + (int64_t)s * L);
+        const float4 v = ld4(p + (int64_t)s * sp);
         a0 += (double)v.x;
         a1 += (double)v.y;
         a2 += (double)v.z;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void reduce_cols4_kernel(const float* __restri
 // in increasing order (4 loads in flight), then a fixed-order tree adds the G group partials.  G
 // is picked so that enough loads are in flight chip-wide (few outputs -> more groups).
 template <int G>
-__global__ __launch_bounds__(512) void reduce_grp4_kernel(const float* __restrict__ part, int S, int64_t L,
+__global__ __launch_bounds__(512) void reduce_grp4_kernel(const float* __restrict__ part, int S, int64_t L, int64_t sp,
                                                           float* __restrict__ out, int64_t row, int64_t ld_out) {
     constexpr int LQ = 512 / G;
     const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
@@ -62,14 +62,14 @@ __global__ __launch_bounds__(512) void reduce_grp4_kernel(const float* __restric
         for (; s + 3 * G < S; s += 4 * G) {
             float4 v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = ld4(part + (int64_t)(s + u * G) * L + l);
+            for (int u = 0; u < 4; ++u) v[u] = ld4(part + (int64_t)(s + u * G) * sp + l);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 a[0] += (double)v[u].x; a[1] += (double)v[u].y; a[2] += (double)v[u].z; a[3] += (double)v[u].w;
             }
         }
         for (; s < S; s += G) {
-            const float4 v0 = ld4(part + (int64_t)s * L + l);
+            const float4 v0 = ld4(part + (int64_t)s * sp + l);
             a[0] += (double)v0.x; a[1] += (double)v0.y; a[2] += (double)v0.z; a[3] += (double)v0.w;
         }
     }
@@ -89,15 +89,47 @@ __global__ __launch_bounds__(512) void reduce_grp4_kernel(const float* __restric
         for (int k = 0; k < 4; ++k) store_out(out, l + k, row, ld_out, red[k][q]);
     }
 }
+// In-place first level for long, narrow reductions (few outputs, many slabs: the single pass would
+// run on a handful of blocks, each walking thousands of slabs): chunk c of CH consecutive slabs is
+// summed (fixed order, double) into its first slab, c * CH, which only this chunk reads.  The
+// second level then reduces the chunk leaders (slab pitch CH * sp).
+__global__ __launch_bounds__(256) void reduce_chunk_kernel(float* __restrict__ part, int S, int64_t L, int64_t sp, int CH) {
+    const int64_t l = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    const int s0 = blockIdx.y * CH, s1 = s0 + CH < S ? s0 + CH : S;
+    if (l >= L) return;
+    float* p = part + (int64_t)s0 * sp + l;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld4(p + (int64_t)(s - s0 + u) * sp);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a0 += (double)v[u].x;
+            a1 += (double)v[u].y;
+            a2 += (double)v[u].z;
+            a3 += (double)v[u].w;
+        }
+    }
+    for (; s < s1; ++s) {
+        const float4 v = ld4(p + (int64_t)(s - s0) * sp);
+        a0 += (double)v.x;
+        a1 += (double)v.y;
+        a2 += (double)v.z;
+        a3 += (double)v.w;
+    }
+    st4(p, make_float4((float)a0, (float)a1, (float)a2, (float)a3));
+}
 // Scalar fallback for L % 4 != 0: block = 64 outputs x 16 slab groups.
-__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L,
+__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L, int64_t sp,
                                                             float* __restrict__ out, int64_t row, int64_t ld_out) {
     constexpr int G = 16;
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int64_t l = (int64_t)blockIdx.x * 64 + lane;
     double acc = 0.0;
     if (l < L)
-        for (int s = g; s < S; s += G) acc += (double)part[(int64_t)s * L + l];
+        for (int s = g; s < S; s += G) acc += (double)part[(int64_t)s * sp + l];
     __shared__ double red[G][64];
     red[g][lane] = acc;
     __syncthreads();
@@ -135,26 +167,37 @@ int check_view(const unet_view* v, const char* op, bool need_vec4) {
     return 0;
 }
 
-int reduce_slabs(const float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream) {
+int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream) {
     UNET_CHECK_ARG(S >= 1 && L >= 1 && row >= 1, "reduce_slabs: bad sizes");
     const bool vec = L % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
+    int64_t sp = L;  // slab pitch
     if (vec) {
         // groups per output quad: enough threads for ~256K loads in flight, at most 32, at most S
         const int64_t quads = L / 4;
+        // long, narrow reductions (< 64 blocks of 16 quads x 32 groups would walk > 256 slabs each):
+        // in-place chunk levels of 16 slabs first
+        while (S > 256 && quads < 64 * 16) {
+            constexpr int CH = 16;
+            const dim3 grid((unsigned)cdiv(quads, 256), (unsigned)cdiv(S, CH));
+            reduce_chunk_kernel<<<grid, 256, 0, stream>>>(part, S, L, sp, CH);
+            UNET_CHECK_LAUNCH("reduce_slabs(chunk)");
+            S = (int)cdiv(S, CH);
+            sp *= CH;
+        }
         int G = 1;
         while (G < 32 && G < S && quads * G < 262144) G *= 2;
         if (G == 1 || S <= 8)
-            reduce_cols4_kernel<<<(unsigned)cdiv(L, 1024), 256, 0, stream>>>(part, S, L, out, row, ld_out);
+            reduce_cols4_kernel<<<(unsigned)cdiv(L, 1024), 256, 0, stream>>>(part, S, L, sp, out, row, ld_out);
         else if (G == 2 || G == 4)
-            reduce_grp4_kernel<4><<<(unsigned)cdiv(quads, 128), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+            reduce_grp4_kernel<4><<<(unsigned)cdiv(quads, 128), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
         else if (G == 8)
-            reduce_grp4_kernel<8><<<(unsigned)cdiv(quads, 64), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+            reduce_grp4_kernel<8><<<(unsigned)cdiv(quads, 64), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
         else if (G == 16)
-            reduce_grp4_kernel<16><<<(unsigned)cdiv(quads, 32), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+            reduce_grp4_kernel<16><<<(unsigned)cdiv(quads, 32), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
         else
-            reduce_grp4_kernel<32><<<(unsigned)cdiv(quads, 16), 512, 0, stream>>>(part, S, L, out, row, ld_out);
+            reduce_grp4_kernel<32><<<(unsigned)cdiv(quads, 16), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
     } else {
-        reduce_slabs_kernel<<<(unsigned)cdiv(L, 64), 1024, 0, stream>>>(part, S, L, out, row, ld_out);
+        reduce_slabs_kernel<<<(unsigned)cdiv(L, 64), 1024, 0, stream>>>(part, S, L, sp, out, row, ld_out);
     }
     UNET_CHECK_LAUNCH("reduce_slabs");
     return 0;
