@@ -246,7 +246,8 @@ def test_pointwise_bwd_data_bnrelu_wgrad(ops, use_bn, m, cout):
 
 
 @pytest.mark.parametrize("use_bn,drop", [(True, 0.0), (True, 0.2), (False, 0.0)])
-@pytest.mark.parametrize("m,cin,cout", [(300, 16, 32), (1000, 64, 128), (257, 128, 64), (128, 4, 8)])
+@pytest.mark.parametrize("m,cin,cout", [(300, 16, 32), (1000, 64, 128), (257, 128, 64), (128, 4, 8),
+                                       (520, 1024, 64)])  # cin >= 1024: dz pass + plain GEMM
 def test_pointwise_bwd_data_bnrelu(ops, use_bn, drop, m, cin, cout):
     """BN + ReLU (+ dropout) backward folded into the pointwise data-gradient GEMM's operand load,
     against the oracle's bn_relu_bwd followed by the pointwise backward."""

@@ -1273,6 +1273,37 @@ extern "C" int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int 
     return launch_rows<A_PLAIN, false, E_STORE>(a, as_stream(stream), "unet_pointwise_bwd_data");
 }
 
+namespace {
+// dz of a BatchNorm + ReLU (+ dropout) block output from (da, z) and coef = (mu, p, q), exactly as
+// the A_BNBWD operand load forms it: one streaming pass (float4 per thread-iteration).
+template <bool DROP>
+__global__ __launch_bounds__(256) void bn_bwd_dz_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                        int64_t M, int C, const float* __restrict__ sc,
+                                                        const float* __restrict__ sh, const float* __restrict__ coef,
+                                                        float rate, float inv_keep, uint64_t seed,
+                                                        float* __restrict__ dz) {
+    const int CQ = C / 4;
+    const int total = (int)(M * CQ);  // < 2^29 (the caller checks M * C < 2^31): 32-bit index math
+    for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+        const int c = (idx % CQ) * 4;
+        const int o = idx * 4;  // = m * C + c
+        float4 v = ld4(da + o);
+        const float4 zz = ld4(z + o), csc = ld4(sc + c), csh = ld4(sh + c);
+        const float4 cmu = ld4(coef + c), cp = ld4(coef + C + c), cq = ld4(coef + 2 * C + c);
+        if constexpr (DROP) v = mul4(v, drop_mult4(seed, (uint64_t)o, rate, inv_keep));
+        v.x = fmaf(zz.x, csc.x, csh.x) > 0.f ? v.x : 0.f;
+        v.y = fmaf(zz.y, csc.y, csh.y) > 0.f ? v.y : 0.f;
+        v.z = fmaf(zz.z, csc.z, csh.z) > 0.f ? v.z : 0.f;
+        v.w = fmaf(zz.w, csc.w, csh.w) > 0.f ? v.w : 0.f;
+        v.x = csc.x * (v.x - cp.x - (zz.x - cmu.x) * cq.x);
+        v.y = csc.y * (v.y - cp.y - (zz.y - cmu.y) * cq.y);
+        v.z = csc.z * (v.z - cp.z - (zz.z - cmu.z) * cq.z);
+        v.w = csc.w * (v.w - cp.w - (zz.w - cmu.w) * cq.w);
+        st4(dz + o, v);
+    }
+}
+}  // namespace
+
 extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout,
                                               const float* pw_kernel, const float* scale, const float* shift,
                                               const float* coef, float drop_rate, uint64_t drop_seed, float* dy,
@@ -1302,6 +1333,32 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
     a.C = dy;
     a.ldc = cin;
     hipStream_t st = as_stream(stream);
+    // The bottleneck-adjacent data gradients (1024 channels on either side: 4+ N-tiles of 256 each
+    // re-forming the same dz tile from (da, z), or 1024-deep k-loops of the BN-backward operand
+    // load) form dz once in a streaming pass (~6 TB/s) and run the plain GEMM on it: 12-24 us
+    // faster per launch (tools/bench_dgrad.py, profiles/r2h_dgrad_split.log); narrower shapes
+    // measured equal or slower that way and keep the fused operand load.
+    if (dz && (cin >= 1024 || cout >= 1024) && cout % 4 == 0 && rows_vec_ok(a, A_BNBWD)) {
+        const int64_t work = m * (cout / 4);
+        const unsigned grid = (unsigned)(work / 256 < 4096 ? cdiv(work, 256) : 4096);
+        if (drop_rate > 0.f)
+            bn_bwd_dz_kernel<true><<<grid, 256, 0, st>>>(da, z, m, cout, scale, shift, coef, drop_rate, a.a.inv_keep,
+                                                         drop_seed, dz);
+        else
+            bn_bwd_dz_kernel<false><<<grid, 256, 0, st>>>(da, z, m, cout, scale, shift, coef, 0.f, 1.f, 0, dz);
+        UNET_CHECK_LAUNCH("unet_pointwise_bwd_data_bnrelu(dz)");
+        RowsArgs p{};
+        p.a = plain_view(dz, cout);
+        p.M = m;
+        p.K = cout;
+        p.B = pw_kernel;
+        p.sbk = 1;
+        p.sbn = cout;
+        p.N = cin;
+        p.C = dy;
+        p.ldc = cin;
+        return launch_rows<A_PLAIN, false, E_STORE>(p, st, "unet_pointwise_bwd_data_bnrelu");
+    }
     if (drop_rate > 0.f)
         return launch_rows<A_BNBWD, true, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
     return launch_rows<A_BNBWD, false, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
