@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 5
+#define UNET_ABI_VERSION 6
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -182,6 +182,21 @@ int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_ke
  * same k-ordered fmaf chain.                                                                  */
 enum { UNET_SEPCONV_AUTO = 0, UNET_SEPCONV_TILE = 1, UNET_SEPCONV_RK = 2 };
 int unet_sepconv_set_schedule(int schedule);
+
+/* Both weight gradients of a SeparableConv2D (model/u_net.py:14-20; the pixel reductions of
+ * Keras' implicit backward, scripts/train.py:308) in one pass WITHOUT the depthwise output y:
+ *   d_pw_kernel[ci, co] = sum_m y[m, ci] * dz[m, co],  y = depthwise3x3(view x) recomputed
+ *   d_dw_kernel[t, ci]  = sum_m x[m + off(t), ci] * dy[m, ci]
+ * so the training forward need not store y (unet_sepconv_fwd with y = NULL).  Replaces
+ * unet_pointwise_bwd_filter over a stored y + unet_dwconv3x3_bwd_filter; both overwritten.
+ * Supported (unet_sepconv_bwd_filter_supported) for the HBM-bound 64 -> 64 blocks: 64 input
+ * and output channels, PLAIN / BNRELU / CONCAT view, h % 8 == 0, w % 16 == 0; dy / dz / the
+ * depthwise kernel / view sources 16-B aligned.                                              */
+int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int h, int w, int cout);
+size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout);
+int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                            const float* dy, const float* dz, int cout, float* d_dw_kernel,
+                            float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream);
 
 /* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
  * momentum 0.99, epsilon 1e-3, biased batch variance for both the output

@@ -510,6 +510,66 @@ def test_sepconv_schedules_bitwise_equal(ops, mode, n, h, w, c0, c1, cout, drop)
     assert rel_err(p1[:nb].double().numpy(), p2[:nb].double().numpy()) < 1e-6
 
 
+SW_CASES = [
+    # mode, n, h, w, c0, c1, drop (64 -> 64 blocks)
+    (1, 2, 8, 16, 64, 0, 0.0),
+    (1, 1, 16, 32, 64, 0, 0.2),      # dropout on the view
+    (0, 2, 8, 32, 64, 0, 0.0),
+    (3, 1, 16, 16, 32, 32, 0.2),     # concat view (decoder), dropout
+    (3, 2, 8, 16, 36, 28, 0.0),      # concat with a quad boundary inside the first source
+    (1, 3, 64, 96, 64, 0, 0.0),      # several tiles per block, ragged tiles per block
+]
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,drop", SW_CASES)
+def test_sepconv_bwd_filter(ops, mode, n, h, w, c0, c1, drop):
+    """Depthwise + pointwise kernel gradients in one pass with y recomputed from the view, against
+    the float64 oracle (y = depthwise(view); d_pw = y^T dz; d_dw from depthwise3x3_bwd), and
+    against the separate route over the y the fused forward stores."""
+    cout = 64
+    rng = np.random.default_rng(500 + mode + n)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = f32(rng.standard_normal((3, 3, C, 1)))
+    dy = f32(rng.standard_normal((n, h, w, C)))
+    dz = f32(rng.standard_normal((n, h, w, cout)))
+    v = _mk_view(ops, mode, t, drop, 41)
+    assert ops.sepconv_bwd_filter_supported(v, n, h, w, cout)
+    ddk = torch.empty((3, 3, C, 1), device="cuda")
+    dpk = torch.empty((1, 1, C, cout), device="cuda")
+    ops.sepconv_bwd_filter(v, n, h, w, dev(dk), dev(dy), dev(dz), cout, ddk, dpk)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"),
+                    drop, 41).astype(np.float64)
+    yr = K.depthwise3x3(xv, dk.astype(np.float64))
+    _, rpk = K.pointwise_bwd(yr, np.zeros((1, 1, C, cout)), dz.astype(np.float64))
+    _, rdk = K.depthwise3x3_bwd(xv, dk.astype(np.float64), dy.astype(np.float64))
+    assert rel_err(host(dpk), rpk) < 1e-5
+    assert rel_err(host(ddk), rdk) < 1e-5
+    y = torch.empty((n, h, w, C), device="cuda")
+    ops.sepconv_fwd(v, n, h, w, dev(dk), cout, dev(f32(rng.standard_normal((1, 1, C, cout)))), y,
+                    torch.empty((n, h, w, cout), device="cuda"))
+    g_pk = torch.empty((1, 1, C, cout), device="cuda")
+    g_dk = torch.empty((3, 3, C, 1), device="cuda")
+    ops.pointwise_bwd_filter(y, dev(dz), n * h * w, C, cout, g_pk)
+    ops.dwconv3x3_bwd_filter(v, n, h, w, dev(dy), g_dk)
+    assert rel_err(host(dpk), host(g_pk)) < 2e-6
+    assert rel_err(host(ddk), host(g_dk)) < 2e-6
+
+
+def test_sepconv_bwd_filter_unsupported(ops):
+    sc = torch.ones(64, device="cuda")
+    x64 = torch.zeros((1, 8, 16, 64), device="cuda")
+    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(torch.zeros((1, 8, 16, 128), device="cuda")),
+                                                1, 8, 16, 64)  # 128 input channels
+    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(x64), 1, 8, 16, 128)  # 128 outputs
+    assert not ops.sepconv_bwd_filter_supported(ops.View.pool_bnrelu(torch.zeros((1, 16, 32, 64), device="cuda"),
+                                                                     sc, sc), 1, 8, 16, 64)
+    with pytest.raises(Exception):
+        ops.sepconv_bwd_filter(ops.View.plain(x64), 1, 8, 16, torch.zeros(9 * 64, device="cuda"),
+                               torch.zeros(8 * 16 * 64, device="cuda"), torch.zeros(8 * 16 * 128, device="cuda"), 128,
+                               torch.empty(9 * 64, device="cuda"), torch.empty(64 * 128, device="cuda"))
+
+
 def test_sepconv_schedule_rk_refuses_narrow(ops):
     """The register-A kernel needs >= 64 input and output channels; forcing it elsewhere errors."""
     x = torch.zeros((1, 8, 16, 4), device="cuda")

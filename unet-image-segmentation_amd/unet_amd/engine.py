@@ -72,6 +72,7 @@ class BlockBufs:
     bnpart: Optional[torch.Tensor] = None  # BN-backward partial sums emitted by the producer of da
     bn_slabs: int = 0  # > 0: bnpart holds this many fresh slabs for the next backward of the block
     bnpart_s: int = -1  # the slab count bnpart's counters were last laid out for
+    y_recompute: bool = False  # last training forward kept no y: the weight grads recompute it
 
 
 @dataclass
@@ -150,6 +151,10 @@ class UNetEngine:
         # image block (4 padded channels): data and pointwise weight gradient in one streaming pass over
         # (da, z, y) that forms dz on the fly, so dz (M x 64) is neither stored nor re-read
         self.img_fused_wgrad = True
+        # weight gradients of the HBM-bound 64 -> 64 blocks in one pass that recomputes the
+        # depthwise output y from the block's input view (unet_sepconv_bwd_filter), so their
+        # forward never stores y
+        self.recompute_y = os.environ.get("UNET_RECOMPUTE_Y", "1") != "0"
         self._ev = None  # created on first use (on the device)
 
     # ------------------------------------------------------------------ weights ------
@@ -251,9 +256,13 @@ class UNetEngine:
         dk, pk = self._wts(b)
         fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= 64 * 64)
         if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
-            # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight grad
+            # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
+            # grads unless they recompute it from the view
             stats = training and self.use_bn
-            ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if training else None, bb.z,
+            bb.y_recompute = training and self.recompute_y and \
+                ops.sepconv_bwd_filter_supported(view, n, h, w, b.cout)
+            keep_y = training and not bb.y_recompute
+            ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
                             bb.part if stats else None)
             if stats:
                 ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean,
@@ -261,6 +270,7 @@ class UNetEngine:
             else:
                 ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
             return View.bnrelu(bb.z, bb.scale, bb.shift)
+        bb.y_recompute = False
         ops.dwconv3x3_fwd(view, n, h, w, dk, bb.y)
         if training and self.use_bn:
             ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, bb.part)
@@ -451,6 +461,9 @@ class UNetEngine:
         gdk, gpk = self._gwts(b)
 
         def weight_grads():
+            if bb.y_recompute:  # both kernels' gradients in one pass, y recomputed from view_in
+                ops.sepconv_bwd_filter(view_in, n, h, w, dk, dy, dz, b.cout, gdk, gpk)
+                return
             if not img_wg:  # (the image block's was accumulated by its data-gradient pass)
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
             ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)

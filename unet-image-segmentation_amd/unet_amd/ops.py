@@ -371,6 +371,28 @@ def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tens
           ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _stream())
 
 
+def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
+    vs = x.c_struct()
+    return bool(L.load().unet_sepconv_bwd_filter_supported(ctypes.byref(vs), n, h, w, cout))
+
+
+def sepconv_bwd_filter(x: View, n: int, h: int, w: int, dk: Tensor, dy: Tensor, dz: Tensor, cout: int,
+                       ddk: Tensor, dpk: Tensor):
+    """Depthwise and pointwise kernel gradients in one pass, y recomputed from the view x."""
+    C = x.channels
+    m = n * h * w
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(dy, "dy", m * C)
+    _check(dz, "dz", m * cout)
+    _check(ddk, "d_depthwise_kernel", 9 * C)
+    _check(dpk, "d_pointwise_kernel", C * cout)
+    ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
+    vs = x.c_struct()
+    _call("unet_sepconv_bwd_filter", (2.0 * m * C * cout + 36.0 * m * C,
+                                      x.src_bytes(n, h, w) + 4.0 * (m * C + m * cout)),
+          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dz), cout, _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
+
+
 # ------------------------------------------------------------------ BatchNorm ---
 def bn_finalize(partials: Tensor, m: int, c: int, gamma, beta, eps, momentum, moving_mean, moving_var,
                 update_moving: bool, mean, rstd, scale, shift):
