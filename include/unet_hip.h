@@ -189,9 +189,9 @@ int unet_sepconv_set_schedule(int schedule);
  *   d_dw_kernel[t, ci]  = sum_m x[m + off(t), ci] * dy[m, ci]
  * so the training forward need not store y (unet_sepconv_fwd with y = NULL).  Replaces
  * unet_pointwise_bwd_filter over a stored y + unet_dwconv3x3_bwd_filter; both overwritten.
- * Supported (unet_sepconv_bwd_filter_supported) for the HBM-bound 64 -> 64 blocks: 64 input
- * and output channels, PLAIN / BNRELU / CONCAT view, h % 8 == 0, w % 16 == 0; dy / dz / the
- * depthwise kernel / view sources 16-B aligned.                                              */
+ * Supported (unet_sepconv_bwd_filter_supported) for the HBM-bound 64-output blocks of the
+ * widest level: input channels % 64 == 0, 64 output channels, PLAIN / BNRELU / CONCAT view,
+ * h % 8 == 0, w % 16 == 0; dy / dz / the depthwise kernel / view sources 16-B aligned.       */
 int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int h, int w, int cout);
 size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout);
 int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,

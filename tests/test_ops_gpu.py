@@ -511,22 +511,23 @@ def test_sepconv_schedules_bitwise_equal(ops, mode, n, h, w, c0, c1, cout, drop)
 
 
 SW_CASES = [
-    # mode, n, h, w, c0, c1, drop (64 -> 64 blocks)
-    (1, 2, 8, 16, 64, 0, 0.0),
-    (1, 1, 16, 32, 64, 0, 0.2),      # dropout on the view
-    (0, 2, 8, 32, 64, 0, 0.0),
-    (3, 1, 16, 16, 32, 32, 0.2),     # concat view (decoder), dropout
-    (3, 2, 8, 16, 36, 28, 0.0),      # concat with a quad boundary inside the first source
-    (1, 3, 64, 96, 64, 0, 0.0),      # several tiles per block, ragged tiles per block
+    # mode, n, h, w, c0, c1, cout, drop
+    (1, 2, 8, 16, 64, 0, 64, 0.0),
+    (1, 1, 16, 32, 64, 0, 64, 0.2),      # dropout on the view
+    (0, 2, 8, 32, 64, 0, 64, 0.0),
+    (3, 1, 16, 16, 32, 32, 64, 0.2),     # concat view (decoder), dropout
+    (3, 2, 8, 16, 36, 28, 64, 0.0),      # concat with a quad boundary inside the first source
+    (3, 1, 16, 32, 64, 64, 64, 0.0),     # two ci groups (dec1_block1: 128 -> 64)
+    (3, 1, 8, 16, 128, 128, 64, 0.2),    # four ci groups
+    (1, 3, 64, 96, 64, 0, 64, 0.0),      # several tiles per block, ragged tiles per block
 ]
 
 
-@pytest.mark.parametrize("mode,n,h,w,c0,c1,drop", SW_CASES)
-def test_sepconv_bwd_filter(ops, mode, n, h, w, c0, c1, drop):
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", SW_CASES)
+def test_sepconv_bwd_filter(ops, mode, n, h, w, c0, c1, cout, drop):
     """Depthwise + pointwise kernel gradients in one pass with y recomputed from the view, against
     the float64 oracle (y = depthwise(view); d_pw = y^T dz; d_dw from depthwise3x3_bwd), and
     against the separate route over the y the fused forward stores."""
-    cout = 64
     rng = np.random.default_rng(500 + mode + n)
     a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
     C = c0 + c1
@@ -559,15 +560,15 @@ def test_sepconv_bwd_filter(ops, mode, n, h, w, c0, c1, drop):
 def test_sepconv_bwd_filter_unsupported(ops):
     sc = torch.ones(64, device="cuda")
     x64 = torch.zeros((1, 8, 16, 64), device="cuda")
-    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(torch.zeros((1, 8, 16, 128), device="cuda")),
-                                                1, 8, 16, 64)  # 128 input channels
+    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(torch.zeros((1, 8, 16, 96), device="cuda")),
+                                                1, 8, 16, 64)  # 96 input channels: not a multiple of 64
     assert not ops.sepconv_bwd_filter_supported(ops.View.plain(x64), 1, 8, 16, 128)  # 128 outputs
     assert not ops.sepconv_bwd_filter_supported(ops.View.pool_bnrelu(torch.zeros((1, 16, 32, 64), device="cuda"),
                                                                      sc, sc), 1, 8, 16, 64)
     with pytest.raises(Exception):
         ops.sepconv_bwd_filter(ops.View.plain(x64), 1, 8, 16, torch.zeros(9 * 64, device="cuda"),
-                               torch.zeros(8 * 16 * 64, device="cuda"), torch.zeros(8 * 16 * 128, device="cuda"), 128,
-                               torch.empty(9 * 64, device="cuda"), torch.empty(64 * 128, device="cuda"))
+                               torch.zeros(8 * 16 * 64, device="cuda"), torch.zeros(8 * 16 * 256, device="cuda"), 256,
+                               torch.empty(9 * 64, device="cuda"), torch.empty(64 * 256, device="cuda"))
 
 
 def test_sepconv_schedule_rk_refuses_narrow(ops):

@@ -29,46 +29,58 @@ namespace unet {
 namespace {
 
 constexpr int TH = 8, TW = 16, HWp = TW + 2, HPIX = (TH + 2) * HWp;  // 180 halo pixels
-constexpr int CI = 64, CO = 64;                                       // channels
+constexpr int CI = 64;                                                // input channels per block (ci group)
 constexpr int NT = 512;                                               // threads
 constexpr int NHQ = HPIX * (CI / 4);                                  // halo float4 (2880)
 constexpr int HR = (NHQ + NT - 1) / NT;                               // per thread (6)
-constexpr int DQ = 128 * CO / 4 / NT;                                 // dz float4 per thread (4)
-constexpr int LDS_HALO = HPIX * CI, LDS_YT = 128 * CI, LDS_DZ = 128 * CO;
-constexpr int LDS_SIZE = LDS_HALO + LDS_YT + LDS_DZ;                  // 110 KB
-static_assert(2 * 64 * 64 <= LDS_SIZE && 9 * 32 * 16 * 4 <= LDS_SIZE, "epilogue scratch");
+constexpr int LDS_HALO = HPIX * CI, LDS_YT = 128 * CI;
+template <int CO>
+struct SwLds {
+    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * CO;  // 110 KB (CO 64) / 142 KB (CO 128)
+    static_assert(64 * 64 * 2 <= SIZE && 9 * 32 * 16 * 4 <= SIZE, "epilogue scratch");
+};
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
 struct SwArgs {
     DView x;
-    int N, H, W;
-    const float* dk;  // (3,3,64,1)
-    const float* dy;  // (M, 64)
-    const float* dz;  // (M, 64)
-    float* pw_slab;   // [S][64][64]
-    float* dw_slab;   // [S][9][64]
-    int tiles, tps;   // pixel tiles, tiles per block
+    int N, H, W, Cin;
+    const float* dk;  // (3,3,Cin,1)
+    const float* dy;  // (M, Cin)
+    const float* dz;  // (M, CO)
+    float* pw_slab;   // [S][Cin][CO]
+    float* dw_slab;   // [S][9][Cin]
+    int tiles, tps;   // pixel tiles, tiles per m-slice
+    int ncig;         // ci groups of 64 channels
 };
 
-template <int MODE, bool DROP>
-__global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
-    __shared__ __attribute__((aligned(16))) float smem[LDS_SIZE];
+template <int MODE, bool DROP, int CO>
+__global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
+    constexpr int DQ = 128 * CO / 4 / NT;  // dz float4 per thread per tile (4 / 8)
+    constexpr int NQ = 2 * (CO / 32);      // (32 ci x 32 co) quarters of the block's 64 x CO output
+    constexpr int PP = 8 / NQ;             // waves per quarter (pixel parts of the tile)
+    constexpr int KS = 64 / PP;            // MFMA k-steps (pixel pairs) per wave per tile
+    __shared__ __attribute__((aligned(16))) float smem[SwLds<CO>::SIZE];
     float* Xs = smem;
     float* Ys = smem + LDS_HALO;
     float* Zs = smem + LDS_HALO + LDS_YT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
-    const int t_begin = blockIdx.x * g.tps;
+    // XCD-aware block -> (ci group, m-slice): blocks b and b + 8 run on one XCD; the ci groups of
+    // an m-slice get consecutive j = b >> 3 there, so they share its dz tiles through that L2
+    const int j = blockIdx.x >> 3;
+    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
+    const int c0 = CI * cig;
+    const int t_begin = slice * g.tps;
     const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
     const int tiles_w = g.W / TW, tiles_h = g.H / TH;
-    const int C = g.x.C;
+    const int C = g.x.C, Cin = g.Cin;
 
     // this thread's channel quad (halo staging, y and filter-gradient quads alike)
-    const int cq = tid & 15, ci = 4 * cq;
+    const int cq = tid & 15, ci = c0 + 4 * cq;
     float4 kt[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * CI + ci);
+    for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
     const float* src = g.x.src0;
     int cs = g.x.c0, cc = ci;
     const float* scp = g.x.sc0;
@@ -108,8 +120,8 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
         }
         const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
 #pragma unroll
-        for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e >> 4, quad e & 15
-            const int e = tid + NT * k, p = e >> 4, q = e & 15;
+        for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e / (CO/4), quad e % (CO/4)
+            const int e = tid + NT * k, p = e / (CO / 4), q = e % (CO / 4);
             rz[k] = ld4(g.dz + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q);
         }
     };
@@ -120,7 +132,7 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int p = (tid >> 4) + 32 * k;
-            rdy[k] = ld4(g.dy + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CI + ci);
+            rdy[k] = ld4(g.dy + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * Cin + ci);
         }
     };
     auto store = [&]() {
@@ -141,13 +153,14 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {
             const int e = tid + NT * k;
-            *reinterpret_cast<float4*>(&Zs[(e >> 4) * CO + 4 * (e & 15)]) = rz[k];
+            *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
         }
     };
 
-    // MFMA quarter of this wave: ci rows 32 (w & 1) .., co columns 32 ((w >> 1) & 1) .., pixels
-    // 64 (w >> 2) .. +63 of the tile (32 k-steps of 2)
-    const int wci = 32 * (wave & 1), wco = 32 * ((wave >> 1) & 1), wpx = 64 * (wave >> 2);
+    // MFMA quarter of this wave: ci rows 32 (q & 1) .., co columns 32 (q >> 1) .. of q = w % NQ,
+    // over pixel part w / NQ of the tile (KS k-steps of 2 pixels)
+    const int qd = wave % NQ;
+    const int wci = 32 * (qd & 1), wco = 32 * (qd >> 1), wpx = 2 * KS * (wave / NQ);
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -175,32 +188,33 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
             for (int dy_ = 0; dy_ < 3; ++dy_)
 #pragma unroll
                 for (int dx_ = 0; dx_ < 3; ++dx_) {
-                    const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + ci]);
+                    const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
                     y = fma4(xv, kt[dy_ * 3 + dx_], y);
                     dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
                 }
-            *reinterpret_cast<float4*>(&Ys[p * CI + ci]) = y;
+            *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
         }
         load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
         __syncthreads();
 #pragma unroll 4
-        for (int s = 0; s < 32; ++s) {
+        for (int s = 0; s < KS; ++s) {
             const int p = wpx + 2 * s + hi;
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[p * CI + wci + lo], Zs[p * CO + wco + lo], acc, 0, 0, 0);
         }
         __syncthreads();
     }
 
-    // pointwise slab [ci][co]: the two pixel halves of each (ci, co) quarter, fixed order
-    float* E = smem;  // [2 pixel halves][64 ci][64 co]
+    // pointwise slab rows c0 .. c0+63: the PP pixel parts of each quarter, fixed order
+    float* E = smem;  // [PP][64 ci][CO]
 #pragma unroll
-    for (int r = 0; r < 16; ++r) E[((wave >> 2) * 64 + wci + acc_row(r, hi)) * CO + wco + lo] = acc[r];
+    for (int r = 0; r < 16; ++r) E[((wave / NQ) * CI + wci + acc_row(r, hi)) * CO + wco + lo] = acc[r];
     __syncthreads();
-    float* pw = g.pw_slab + (int64_t)blockIdx.x * CI * CO;
+    float* pw = g.pw_slab + ((int64_t)slice * Cin + c0) * CO;
     for (int e = tid; e < CI * CO / 4; e += NT) {
-        const float4 a = *reinterpret_cast<const float4*>(&E[4 * e]);
-        const float4 b = *reinterpret_cast<const float4*>(&E[CI * CO + 4 * e]);
-        st4(pw + 4 * e, add4(a, b));
+        float4 a = *reinterpret_cast<const float4*>(&E[4 * e]);
+#pragma unroll
+        for (int pp = 1; pp < PP; ++pp) a = add4(a, *reinterpret_cast<const float4*>(&E[pp * CI * CO + 4 * e]));
+        st4(pw + 4 * e, a);
     }
     __syncthreads();
     // depthwise slab [t][ci]: the 32 threads of each channel quad, fixed-order tree
@@ -215,8 +229,8 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad64_kernel(SwArgs g) {
         }
         __syncthreads();
     }
-    float* dws = g.dw_slab + (int64_t)blockIdx.x * 9 * CI;
-    if (tid < 9 * 16) st4(dws + (tid / 16) * CI + 4 * (tid % 16), D[(tid / 16) * 32 * 16 + (tid % 16)]);
+    float* dws = g.dw_slab + (int64_t)slice * 9 * Cin;
+    if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 32 * 16 + (tid % 16)]);
 }
 
 int resident_cus() {
@@ -231,20 +245,23 @@ int resident_cus() {
 }
 
 struct SwPlan {
-    int tiles, S, tps;
+    int tiles, ncig, S, tps;
 };
-SwPlan sw_plan(int n, int h, int w) {
+SwPlan sw_plan(int n, int h, int w, int cin) {
     SwPlan p;
     p.tiles = n * (h / TH) * (w / TW);
-    const int cus = resident_cus();
-    p.tps = (int)cdiv(p.tiles, cus);  // one block per CU (110 KB of LDS)
-    p.S = (int)cdiv(p.tiles, p.tps);
+    p.ncig = cin / CI;
+    // one block per CU (110-142 KB of LDS): m-slices a multiple of 8 (the XCD map)
+    int S = (int)cdiv(resident_cus(), p.ncig);
+    S = (int)cdiv(S, 8) * 8;
+    p.tps = (int)cdiv(p.tiles, S);
+    p.S = S;
     return p;
 }
 
 template <int MODE, bool DROP>
-void launch_sw(const SwArgs& a, int blocks, hipStream_t st) {
-    sepconv_wgrad64_kernel<MODE, DROP><<<blocks, NT, 0, st>>>(a);
+void launch_sw(const SwArgs& a, int, int blocks, hipStream_t st) {
+    sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
 }
 
 }  // namespace
@@ -253,18 +270,22 @@ void launch_sw(const SwArgs& a, int blocks, hipStream_t st) {
 using namespace unet;
 
 extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int h, int w, int cout) {
-    if (!x || n <= 0 || h <= 0 || w <= 0 || cout != CO) return 0;
+    // 64 outputs: the 256 x 256 level.  The 128-output kernel (the 128 x 128 level) measured slower
+    // than the separate launches there (224 vs 188 us; tools/bench_sepwgrad.py), so it is not offered.
+    if (!x || n <= 0 || h <= 0 || w <= 0 || cout != 64) return 0;
     if (x->mode != UNET_VIEW_PLAIN && x->mode != UNET_VIEW_BNRELU && x->mode != UNET_VIEW_CONCAT) return 0;
     const int C = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
-    if (C != CI || h % TH || w % TW) return 0;
+    if (C % CI || h % TH || w % TW) return 0;
     if (x->mode == UNET_VIEW_CONCAT && x->c0 % 4) return 0;
-    return (int64_t)n * h * w * CI < (int64_t(1) << 31);
+    const int64_t M = (int64_t)n * h * w;
+    return M * C < (int64_t(1) << 31) && M * cout < (int64_t(1) << 31);
 }
 
 extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout) {
-    if (n <= 0 || h <= 0 || w <= 0 || cin != CI || cout != CO || h % TH || w % TW) return 0;
-    const SwPlan p = sw_plan(n, h, w);
-    return align_up((size_t)p.S * CI * CO * sizeof(float), 256) + align_up((size_t)p.S * 9 * CI * sizeof(float), 256);
+    if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || cout != 64 || h % TH || w % TW)
+        return 0;
+    const SwPlan p = sw_plan(n, h, w, cin);
+    return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
 }
 
 extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,
@@ -272,45 +293,50 @@ extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, 
                                        float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
     if (check_view(x, "unet_sepconv_bwd_filter")) return -1;
     UNET_CHECK_ARG(unet_sepconv_bwd_filter_supported(x, n, h, w, cout),
-                   "unet_sepconv_bwd_filter: unsupported shape (needs 64 input and output channels, a PLAIN / "
-                   "BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
+                   "unet_sepconv_bwd_filter: unsupported shape (needs input channels %% 64 == 0, 64 output "
+                   "channels, a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
     UNET_CHECK_ARG(dw_kernel && dy && dz && d_dw_kernel && d_pw_kernel, "unet_sepconv_bwd_filter: null pointer");
     UNET_CHECK_ARG(((uintptr_t)dy | (uintptr_t)dz | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
                     (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
                    "unet_sepconv_bwd_filter: operands must be 16-B aligned");
-    const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, CI, CO);
+    const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
+    const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_sepconv_bwd_filter: workspace %zu < %zu", ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w);
+    const SwPlan p = sw_plan(n, h, w, cin);
     SwArgs a{};
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;
     a.W = w;
+    a.Cin = cin;
     a.dk = dw_kernel;
     a.dy = dy;
     a.dz = dz;
     a.pw_slab = static_cast<float*>(ws);
-    a.dw_slab = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)p.S * CI * CO * sizeof(float), 256));
+    a.dw_slab = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)p.S * cin * cout * sizeof(float), 256));
     a.tiles = p.tiles;
     a.tps = p.tps;
+    a.ncig = p.ncig;
+    const int blocks = p.S * p.ncig;
     hipStream_t st = as_stream(stream);
     const bool drop = x->drop_rate > 0.f;
     switch (x->mode) {
         case UNET_VIEW_PLAIN:
-            if (drop) launch_sw<UNET_VIEW_PLAIN, true>(a, p.S, st);
-            else launch_sw<UNET_VIEW_PLAIN, false>(a, p.S, st);
+            if (drop) launch_sw<UNET_VIEW_PLAIN, true>(a, cout, blocks, st);
+            else launch_sw<UNET_VIEW_PLAIN, false>(a, cout, blocks, st);
             break;
         case UNET_VIEW_BNRELU:
-            if (drop) launch_sw<UNET_VIEW_BNRELU, true>(a, p.S, st);
-            else launch_sw<UNET_VIEW_BNRELU, false>(a, p.S, st);
+            if (drop) launch_sw<UNET_VIEW_BNRELU, true>(a, cout, blocks, st);
+            else launch_sw<UNET_VIEW_BNRELU, false>(a, cout, blocks, st);
             break;
         default:
-            if (drop) launch_sw<UNET_VIEW_CONCAT, true>(a, p.S, st);
-            else launch_sw<UNET_VIEW_CONCAT, false>(a, p.S, st);
+            if (drop) launch_sw<UNET_VIEW_CONCAT, true>(a, cout, blocks, st);
+            else launch_sw<UNET_VIEW_CONCAT, false>(a, cout, blocks, st);
             break;
     }
     UNET_CHECK_LAUNCH("unet_sepconv_bwd_filter");
-    int rc = reduce_slabs(a.pw_slab, p.S, (int64_t)CI * CO, d_pw_kernel, (int64_t)CI * CO, (int64_t)CI * CO, st);
+    const int64_t lp = (int64_t)cin * cout, ld = (int64_t)9 * cin;
+    int rc = reduce_slabs(a.pw_slab, p.S, lp, d_pw_kernel, lp, lp, st);
     if (rc) return rc;
-    return reduce_slabs(a.dw_slab, p.S, (int64_t)9 * CI, d_dw_kernel, (int64_t)9 * CI, (int64_t)9 * CI, st);
+    return reduce_slabs(a.dw_slab, p.S, ld, d_dw_kernel, ld, ld, st);
 }
