@@ -72,7 +72,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
     step) at `batch` images, each timed with HIP events (median of `reps`), against
     t_roof = max(flops / peak_fp32, bytes / peak_hbm) with flops = px(18 Cin + 2 Cin Cout) and
     bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Uses the engine's kernel choice
-    (fused unet_sepconv_fwd where supported, dw + pw launches for the 3-channel first block)."""
+    (fused unet_sepconv_fwd where supported, dw + pw launches for the 3-channel first block), and
+    stores the depthwise output y only where the train step does."""
     import torch
     from unet_amd import ops
     from unet_amd.ops import View
@@ -95,6 +96,9 @@ def encoder_block_roofline(batch, size, device, reps=10):
             dk = torch.randn((3, 3, ck, 1), generator=g).to(device)
             pk = (torch.randn((1, 1, ck, co), generator=g) / ci ** 0.5).to(device)
             m = batch * hh * hh
+            # y (the depthwise output) is stored only where the train step keeps it: blocks whose
+            # weight gradients recompute it from the view (unet_sepconv_bwd_filter) do not
+            keep_y = not ops.sepconv_bwd_filter_supported(view, batch, hh, hh, co)
             ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
             part = torch.zeros(ops.bn_partials_numel(m, co), device=device)
@@ -102,7 +106,7 @@ def encoder_block_roofline(batch, size, device, reps=10):
 
             def run():
                 if fused:
-                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf, z, part)
+                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf if keep_y else None, z, part)
                 else:
                     ops.dwconv3x3_fwd(view, batch, hh, hh, dk, ybuf)
                     ops.pointwise_fwd(ybuf, m, ck, co, pk, z, part)

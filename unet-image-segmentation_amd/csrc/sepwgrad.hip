@@ -28,6 +28,9 @@
 namespace unet {
 namespace {
 
+#ifndef SW_KO  // lab knock-outs (tools/lab/sw_lab.hip): 1 MFMA, 2 depthwise VALU, 4 loop loads, 8 LDS staging
+#define SW_KO 0
+#endif
 constexpr int TH = 8, TW = 16, HWp = TW + 2, HPIX = (TH + 2) * HWp;  // 180 halo pixels
 constexpr int CI = 64;                                                // input channels per block (ci group)
 constexpr int NT = 512;                                               // threads
@@ -173,11 +176,11 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         load_dy(t_begin);
     }
     for (int T = t_begin; T < t_end; ++T) {
-        store();
+        if constexpr (!(SW_KO & 8)) store();
         __syncthreads();
-        load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
+        if constexpr (!(SW_KO & 4)) load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
 #pragma unroll 1
-        for (int k = 0; k < 4; ++k) {  // (not unrolled: 9 taps in flight, not 36)
+        for (int k = 0; k < ((SW_KO & 2) ? 0 : 4); ++k) {  // (not unrolled: 9 taps in flight, not 36)
             const int p = (tid >> 4) + 32 * k, pr = p >> 4, pc = p & 15;
             const float4 dq = rdy[0];  // static register indexing: rotate the dy quads
             rdy[0] = rdy[1];
@@ -194,10 +197,10 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
                 }
             *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
         }
-        load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
+        if constexpr (!(SW_KO & 4)) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
         __syncthreads();
 #pragma unroll 4
-        for (int s = 0; s < KS; ++s) {
+        for (int s = 0; s < ((SW_KO & 1) ? 0 : KS); ++s) {
             const int p = wpx + 2 * s + hi;
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[p * CI + wci + lo], Zs[p * CO + wco + lo], acc, 0, 0, 0);
         }
