@@ -69,7 +69,8 @@ def op_breakdown(summary):
 def encoder_block_roofline(batch, size, device, reps=10):
     """forward, training-mode conv blocks of the encoder (depthwise -> pointwise +
     BN-statistics epilogue; the BN apply + ReLU of the input is done on load, as in the train
-    step) at `batch` images, each timed with HIP events (median of `reps`), against
+    step) at `batch` images, each timed with HIP events around `reps` back-to-back launches (median
+    of 3 groups), against
     t_roof = max(flops / peak_fp32, bytes / peak_hbm) with flops = px(18 Cin + 2 Cin Cout) and
     bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Uses the engine's kernel choice
     (fused unet_sepconv_fwd where supported, dw + pw launches for the 3-channel first block), and
