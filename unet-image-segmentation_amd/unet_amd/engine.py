@@ -155,6 +155,12 @@ class UNetEngine:
         # depthwise output y from the block's input view (unet_sepconv_bwd_filter), so their
         # forward never stores y
         self.recompute_y = os.environ.get("UNET_RECOMPUTE_Y", "1") != "0"
+        # issue a y-recomputing block's fused weight gradient (one 111 KB-LDS block per CU for the
+        # launch's whole length) only after the main stream has issued the NEXT block's statistics
+        # finish, instead of beside its own depthwise data gradient (single-process runs only: with
+        # a gradient hook the all-reduce low-water mark must not overtake it)
+        self.defer_sw = os.environ.get("UNET_SW_DEFER", "0") != "0"
+        self._pending_side = None
         self._ev = None  # created on first use (on the device)
 
     # ------------------------------------------------------------------ weights ------
@@ -393,6 +399,14 @@ class UNetEngine:
         else:
             self._ev.wait(main, self.side)
 
+    def _flush_side(self):
+        """Issue the deferred side-stream weight gradients (UNET_SW_DEFER), if any."""
+        if self._pending_side is not None:
+            fn, self._pending_side = self._pending_side, None
+            self._side_wait_main()
+            with torch.cuda.stream(self.side):
+                fn()
+
     def _grads_ready(self, name: str):
         """Gradients at flat offsets >= offset(name) are final once both streams get here:
         the hook (bucketed all-reduce) is issued from the side stream after it has caught up
@@ -447,6 +461,7 @@ class UNetEngine:
                 ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
+            self._flush_side()
             img_wg = self.img_fused_wgrad and drop_rate == 0.0 and b.cin == 4 and b.cout in (32, 64)
             if img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
                 ops.pointwise_bwd_data_bnrelu_wgrad(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
@@ -474,9 +489,13 @@ class UNetEngine:
         # the image block (dx0 None) has no data gradient after this: its weight gradients run
         # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
         if self.overlap and dx0 is not None:
-            self._side_wait_main()
-            with torch.cuda.stream(self.side):
-                weight_grads()
+            self._flush_side()
+            if self.defer_sw and bb.y_recompute and self.grad_hook is None:
+                self._pending_side = weight_grads
+            else:
+                self._side_wait_main()
+                with torch.cuda.stream(self.side):
+                    weight_grads()
         else:
             weight_grads()
         if dx0 is not None:
@@ -570,6 +589,7 @@ class UNetEngine:
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
+        self._flush_side()
         if self.overlap:
             self._main_wait_side()
 
