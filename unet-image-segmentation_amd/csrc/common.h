@@ -43,9 +43,10 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 // Wave issue priority of the critical-path (main-stream) backward kernels: while the weight
 // gradients run beside them on a second stream, their waves win the SIMD's instruction
-// arbitration (s_setprio; 0 = the default, equal priority).  Build-time choice (UNET_MAIN_PRIO).
+// arbitration (s_setprio; 0 = equal priority).  Build-time choice (UNET_MAIN_PRIO); 3 measured
+// +0.7-1.0 % img/s against 0 (round 2, tools/gpu_x1.sh / gpu_x2.sh A/B on one box).
 #ifndef UNET_MAIN_PRIO
-#define UNET_MAIN_PRIO 0
+#define UNET_MAIN_PRIO 3
 #endif
 __device__ __forceinline__ void main_stream_prio() {
     if constexpr (UNET_MAIN_PRIO > 0) __builtin_amdgcn_s_setprio(UNET_MAIN_PRIO);

@@ -466,12 +466,9 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         const int rr = arow + (256 / KQ) * r;
         if (rr < M_rem) {
             const int m = m0 + rr;
-            if constexpr (AMODE == A_UNSHUFFLE) {
-                const int hw = g.uH * g.uW;
-                const int n = m / hw;
-                const int rem = m - n * hw;
-                const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
-                aoff[r] = ((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf;
+            if constexpr (AMODE == A_UNSHUFFLE) {  // (0, 0) tap of pixel m: dU row 2 (m / uW), column 2 (m % uW)
+                const int ur = m / g.uW;
+                aoff[r] = (4 * ur * g.uW + 2 * (m - ur * g.uW)) * g.uf;
             } else {
                 aoff[r] = m * g.a.c0;
             }
@@ -737,19 +734,21 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         }
     }
     if constexpr (EPI == E_SHUFFLE) {
-        const int hw = g.sH * g.sW;
-        int obase[TM][16];  // output pixel offset (a = b = 0 tap) of each accumulator row
+        // output pixel offset (a = b = 0 tap) of each tile row: one row per thread through LDS
+        // (the loop ended on a barrier) instead of two runtime integer divisions per accumulator
+        // row in every thread (~2000 VALU instructions per thread)
+        int* orow = reinterpret_cast<int*>(&As[0][0]);
+        if (tid < BM) {
+            const int m = m0 + tid;
+            const int ur = m / g.sW;  // image row over the batch; output row 2 ur, column 2 (m % sW)
+            orow[tid] = tid < M_rem ? (4 * ur * g.sW + 2 * (m - ur * g.sW)) * g.sf : -1;
+        }
+        __syncthreads();
+        int obase[TM][16];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int rr = wm * (BM / 2) + tm * 32 + acc_row(r, hi);
-                const int m = m0 + rr;
-                const int img = m / hw;
-                const int rem = m - img * hw;
-                const int i = rem / g.sW, j = rem - (rem / g.sW) * g.sW;
-                obase[tm][r] = rr < M_rem ? ((img * 2 * g.sH + 2 * i) * (2 * g.sW) + 2 * j) * g.sf : -1;
-            }
+            for (int r = 0; r < 16; ++r) obase[tm][r] = orow[wm * (BM / 2) + tm * 32 + acc_row(r, hi)];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
             const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
@@ -822,6 +821,18 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     }
 
     float4 ra[AR], rb[BR];
+    // W_UNSHUFFLE: pixel m = (image row ur = m / uW over the batch, column uj) of the upsample input;
+    // its (0, 0) tap in dU is row 2 ur, column 2 uj.  Tracked incrementally (the stages advance m
+    // by BK) instead of two runtime divisions per row and stage.
+    int ur[AMODE == W_UNSHUFFLE ? AR : 1], uj[AMODE == W_UNSHUFFLE ? AR : 1];
+    if constexpr (AMODE == W_UNSHUFFLE) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r) {
+            const int m = mb + amm + AS * r;
+            ur[r] = m / g.uW;
+            uj[r] = m - ur[r] * g.uW;
+        }
+    }
     auto load_stage = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < AR; ++r) {
@@ -829,11 +840,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
             float4 v = f4(0.f);
             if (pv && m < me) {
                 if constexpr (AMODE == W_UNSHUFFLE) {
-                    const int hw = g.uH * g.uW;
-                    const int n = m / hw;
-                    const int rem = m - n * hw;
-                    const int i = rem / g.uW, j = rem - (rem / g.uW) * g.uW;
-                    v = ld4(g.a.src0 + ((n * 2 * g.uH + 2 * i) * 2 * g.uW + 2 * j) * g.uf + poff);
+                    v = ld4(g.a.src0 + (4 * ur[r] * g.uW + 2 * uj[r]) * g.uf + poff);
                 } else {
                     v = ld4(g.a.src0 + (int64_t)m * g.a.c0 + p);
                     if constexpr (AMODE == W_BNRELU) v = bnrelu4(v, asc, ash);
@@ -869,6 +876,16 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
                 }
             }
             rb[r] = v;
+        }
+        if constexpr (AMODE == W_UNSHUFFLE) {
+#pragma unroll
+            for (int r = 0; r < AR; ++r) {
+                uj[r] += BK;
+                while (uj[r] >= g.uW) {
+                    uj[r] -= g.uW;
+                    ++ur[r];
+                }
+            }
         }
     };
     const bool csum_on = g.colpart != nullptr && (int)blockIdx.x < ntp;  // q-tile 0 blocks sum A's columns

@@ -159,7 +159,7 @@ class UNetEngine:
         # launch's whole length) only after the main stream has issued the NEXT block's statistics
         # finish, instead of beside its own depthwise data gradient (single-process runs only: with
         # a gradient hook the all-reduce low-water mark must not overtake it)
-        self.defer_sw = os.environ.get("UNET_SW_DEFER", "0") != "0"
+        self.defer_sw = os.environ.get("UNET_SW_DEFER", "1") != "0"
         self._pending_side = None
         self._ev = None  # created on first use (on the device)
 
