@@ -520,6 +520,8 @@ SW_CASES = [
     (3, 1, 16, 32, 64, 64, 64, 0.0),     # two ci groups (dec1_block1: 128 -> 64)
     (3, 1, 8, 16, 128, 128, 64, 0.2),    # four ci groups
     (1, 3, 64, 96, 64, 0, 64, 0.0),      # several tiles per block, ragged tiles per block
+    (1, 2, 16, 32, 128, 0, 128, 0.0),    # 128 outputs (the 128 x 128 level: enc2_block2 / dec2_block2)
+    (3, 1, 16, 32, 128, 128, 128, 0.2),  # 128 outputs, concat + dropout (dec2_block1: 256 -> 128)
 ]
 
 
@@ -562,7 +564,7 @@ def test_sepconv_bwd_filter_unsupported(ops):
     x64 = torch.zeros((1, 8, 16, 64), device="cuda")
     assert not ops.sepconv_bwd_filter_supported(ops.View.plain(torch.zeros((1, 8, 16, 96), device="cuda")),
                                                 1, 8, 16, 64)  # 96 input channels: not a multiple of 64
-    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(x64), 1, 8, 16, 128)  # 128 outputs
+    assert not ops.sepconv_bwd_filter_supported(ops.View.plain(x64), 1, 8, 16, 256)  # 256 outputs
     assert not ops.sepconv_bwd_filter_supported(ops.View.pool_bnrelu(torch.zeros((1, 16, 32, 64), device="cuda"),
                                                                      sc, sc), 1, 8, 16, 64)
     with pytest.raises(Exception):

@@ -1,12 +1,15 @@
-"""Per-launch listing of ONE training step from a rocprofv3 kernel-trace CSV (the last complete
-step: between the last two AdamW launches), with durations, grid and resource usage, and a
+"""Per-launch listing of ONE training step from a rocprofv3 kernel-trace CSV (the complete step
+of median wall time: between two AdamW launches), with durations, grid and resource usage, and a
 per-kernel-family total.  usage: python tools/step_trace.py trace.csv [min_us]"""
 import csv, re, sys
 from collections import defaultdict
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ad = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
-a, b = ad[-2] + 1, ad[-1] + 1
+# the step of median wall time among the complete steps (the last one can carry host gaps)
+walls = sorted((int(rows[j]["End_Timestamp"]) - int(rows[i + 1]["Start_Timestamp"]), i, j) for i, j in zip(ad, ad[1:]))
+_, i0, j0 = walls[len(walls) // 2]
+a, b = i0 + 1, j0 + 1
 step = rows[a:b]
 t0 = int(step[0]["Start_Timestamp"])
 tend = int(step[-1]["End_Timestamp"])

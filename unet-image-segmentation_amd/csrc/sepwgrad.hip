@@ -1,4 +1,4 @@
-// Weight gradients of a 64 -> 64 SeparableConv2D (reference model/u_net.py:14-20; the pixel
+// Weight gradients of a C -> 64 (or 128) SeparableConv2D (reference model/u_net.py:14-20; the pixel
 // reductions of Keras' implicit backward, scripts/train.py:308) in ONE pass that never reads the
 // depthwise output y:
 //
@@ -263,8 +263,9 @@ SwPlan sw_plan(int n, int h, int w, int cin) {
 }
 
 template <int MODE, bool DROP>
-void launch_sw(const SwArgs& a, int, int blocks, hipStream_t st) {
-    sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
+void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
+    if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
+    else sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
 }
 
 }  // namespace
@@ -273,9 +274,10 @@ void launch_sw(const SwArgs& a, int, int blocks, hipStream_t st) {
 using namespace unet;
 
 extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int h, int w, int cout) {
-    // 64 outputs: the 256 x 256 level.  The 128-output kernel (the 128 x 128 level) measured slower
-    // than the separate launches there (224 vs 188 us; tools/bench_sepwgrad.py), so it is not offered.
-    if (!x || n <= 0 || h <= 0 || w <= 0 || cout != 64) return 0;
+    // 64 outputs (the 256 x 256 level) or 128 (the 128 x 128 level: 142 KB of LDS; isolated it is
+    // slower than the separate launches, 224 vs 188 us in tools/bench_sepwgrad.py, but it lets the
+    // forward skip the y store -- the engine chooses per level)
+    if (!x || n <= 0 || h <= 0 || w <= 0 || (cout != 64 && cout != 128)) return 0;
     if (x->mode != UNET_VIEW_PLAIN && x->mode != UNET_VIEW_BNRELU && x->mode != UNET_VIEW_CONCAT) return 0;
     const int C = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     if (C % CI || h % TH || w % TW) return 0;
@@ -285,7 +287,7 @@ extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int 
 }
 
 extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout) {
-    if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || cout != 64 || h % TH || w % TW)
+    if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || (cout != 64 && cout != 128) || h % TH || w % TW)
         return 0;
     const SwPlan p = sw_plan(n, h, w, cin);
     return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
@@ -296,8 +298,8 @@ extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, 
                                        float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
     if (check_view(x, "unet_sepconv_bwd_filter")) return -1;
     UNET_CHECK_ARG(unet_sepconv_bwd_filter_supported(x, n, h, w, cout),
-                   "unet_sepconv_bwd_filter: unsupported shape (needs input channels %% 64 == 0, 64 output "
-                   "channels, a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
+                   "unet_sepconv_bwd_filter: unsupported shape (needs input channels %% 64 == 0, 64 or 128 "
+                   "output channels, a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
     UNET_CHECK_ARG(dw_kernel && dy && dz && d_dw_kernel && d_pw_kernel, "unet_sepconv_bwd_filter: null pointer");
     UNET_CHECK_ARG(((uintptr_t)dy | (uintptr_t)dz | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
                     (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
