@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 6
+#define UNET_ABI_VERSION 7
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -78,6 +78,13 @@ int unet_event_create(void** event);
 int unet_event_destroy(void* event);
 int unet_stream_wait_stream(unet_stream_t waiter, unet_stream_t producer,
                             void* event);
+
+/* Channel-strided copy: dst[r * dst_ld + c] = src[r * src_ld + c] for r < rows, c < cols.
+ * The image block's 3 -> 4 channel zero padding (model/u_net.py:58 Input of 3 channels; the pad
+ * channel of dst is left as it is) and the Keras-shaped (3, 3, 3, 1) / (1, 1, 3, 64) slices of
+ * its padded kernels and their gradients, so no step copy goes through a framework kernel.   */
+int unet_copy_strided(const float* src, int64_t rows, int cols, int64_t src_ld, float* dst,
+                      int64_t dst_ld, unet_stream_t stream);
 
 /* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
  * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers

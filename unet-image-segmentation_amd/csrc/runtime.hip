@@ -205,6 +205,32 @@ int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t
 
 }  // namespace unet
 
+namespace unet {
+namespace {
+__global__ __launch_bounds__(256) void copy_strided_kernel(const float* __restrict__ src, int64_t rows, int cols,
+                                                           int64_t src_ld, float* __restrict__ dst, int64_t dst_ld) {
+    const int64_t n = rows * cols;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / cols, c = i - r * cols;
+        dst[r * dst_ld + c] = src[r * src_ld + c];
+    }
+}
+}  // namespace
+}  // namespace unet
+
+extern "C" int unet_copy_strided(const float* src, int64_t rows, int cols, int64_t src_ld, float* dst, int64_t dst_ld,
+                                 unet_stream_t stream) {
+    UNET_CHECK_ARG(src && dst, "unet_copy_strided: null pointer");
+    UNET_CHECK_ARG(rows >= 0 && cols >= 0 && src_ld >= cols && dst_ld >= cols, "unet_copy_strided: bad sizes");
+    const int64_t n = rows * cols;
+    if (n == 0) return 0;
+    const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+    unet::copy_strided_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(src, rows, cols, src_ld,
+                                                                                              dst, dst_ld);
+    UNET_CHECK_LAUNCH("unet_copy_strided");
+    return 0;
+}
+
 extern "C" int unet_abi_version(void) { return UNET_ABI_VERSION; }
 extern "C" const char* unet_last_error(void) { return unet::g_err; }
 

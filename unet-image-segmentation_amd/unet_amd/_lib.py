@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -43,6 +43,7 @@ P = c_void_p
 # name -> (restype, argtypes); exactly the entry points of include/unet_hip.h
 SIGNATURES = {
     "unet_abi_version": (c_int, []),
+    "unet_copy_strided": (c_int, [P, c_int64, c_int, c_int64, P, c_int64, P]),
     "unet_last_error": (c_char_p, []),
     "unet_event_create": (c_int, [POINTER(c_void_p)]),
     "unet_event_destroy": (c_int, [P]),

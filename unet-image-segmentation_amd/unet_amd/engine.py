@@ -301,9 +301,9 @@ class UNetEngine:
         if not b.wcin:
             return dk, pk
         pad = self._pad_w
-        if refresh:
-            pad["dk"][:, :, :b.wcin].copy_(dk)
-            pad["pk"][:, :, :b.wcin].copy_(pk)
+        if refresh:  # (3, 3, wcin, 1) -> (3, 3, cin, 1); (1, 1, wcin, cout) -> the first wcin rows
+            ops.copy_strided(dk, 9, b.wcin, b.wcin, pad["dk"], b.cin)
+            ops.copy_strided(pk, 1, b.wcin * b.cout, b.wcin * b.cout, pad["pk"], b.cin * b.cout)
         return pad["dk"], pad["pk"]
 
     def _gwts(self, b: Block):
@@ -331,7 +331,7 @@ class UNetEngine:
         if xp is None or xp.shape[0] != x.shape[0]:
             xp = torch.zeros((x.shape[0], self.h, self.w, self.cpad), dtype=torch.float32, device=self.device)
             A.xpad = xp
-        xp[..., :self.c].copy_(x)
+        ops.copy_strided(x, x.shape[0] * self.h * self.w, self.c, self.c, xp, self.cpad)
         return xp
 
     def drop_seeds(self, step: int) -> Dict[str, int]:
@@ -489,8 +489,9 @@ class UNetEngine:
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
             ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
-                self.gvars[f"{b.name}_sepconv/pointwise_kernel"].copy_(gpk[:, :, :b.wcin])
-                self.gvars[f"{b.name}_sepconv/depthwise_kernel"].copy_(gdk[:, :, :b.wcin])
+                ops.copy_strided(gpk, 1, b.wcin * b.cout, b.cin * b.cout,
+                                 self.gvars[f"{b.name}_sepconv/pointwise_kernel"], b.wcin * b.cout)
+                ops.copy_strided(gdk, 9, b.wcin, b.cin, self.gvars[f"{b.name}_sepconv/depthwise_kernel"], b.wcin)
 
         # the image block (dx0 None) has no data gradient after this: its weight gradients run
         # on the otherwise idle main stream, beside the side stream's enc1_block2 tail

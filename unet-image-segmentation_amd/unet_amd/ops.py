@@ -210,6 +210,15 @@ def view_materialize(x: View, n: int, h: int, w: int, out: Tensor) -> Tensor:
 
 
 # --------------------------------------------------------------- SeparableConv2D ---
+def copy_strided(src: Tensor, rows: int, cols: int, src_ld: int, dst: Tensor, dst_ld: int) -> None:
+    """dst[r * dst_ld + c] = src[r * src_ld + c] (r < rows, c < cols): channel padding / slicing."""
+    _check(src, "src")
+    _check(dst, "dst")
+    if rows and (src.numel() < (rows - 1) * src_ld + cols or dst.numel() < (rows - 1) * dst_ld + cols):
+        raise ValueError("copy_strided: tensors too small for rows x cols at the given strides")
+    _call("unet_copy_strided", (0.0, 8.0 * rows * cols), _ptr(src), rows, cols, src_ld, _ptr(dst), dst_ld, _stream())
+
+
 def dwconv3x3_fwd(x: View, n: int, h: int, w: int, dk: Tensor, out: Tensor) -> Tensor:
     C = x.channels
     _check(dk, "depthwise_kernel", 9 * C)
