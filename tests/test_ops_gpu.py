@@ -778,3 +778,20 @@ def test_dwconv_bwd_fused(ops, mode, n, h, w, c0, c1, drop):
             outs.append((host(dg), host(db), host(coef)))
         for x, y in zip(outs[0], outs[1]):
             assert rel_err(x, y) < 2e-5
+
+
+def test_copy_strided(ops):
+    """Channel padding (3 -> 4, pad channel untouched) and slicing back, bit-exact."""
+    x = torch.randn(2, 8, 16, 3, device="cuda")
+    xp = torch.full((2, 8, 16, 4), 7.0, device="cuda")
+    ops.copy_strided(x, 2 * 8 * 16, 3, 3, xp, 4)
+    assert torch.equal(xp[..., :3], x) and bool((xp[..., 3] == 7.0).all())
+    back = torch.empty(2, 8, 16, 3, device="cuda")
+    ops.copy_strided(xp, 2 * 8 * 16, 3, 4, back, 3)
+    assert torch.equal(back, x)
+    pk = torch.randn(1, 1, 3, 64, device="cuda")
+    pp = torch.zeros(1, 1, 4, 64, device="cuda")
+    ops.copy_strided(pk, 1, 3 * 64, 3 * 64, pp, 4 * 64)
+    assert torch.equal(pp[:, :, :3], pk) and not pp[:, :, 3].any()
+    with pytest.raises(ValueError):
+        ops.copy_strided(x, 2 * 8 * 16, 3, 4, xp, 4)  # source too small for its stride
