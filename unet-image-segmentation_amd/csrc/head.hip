@@ -177,45 +177,66 @@ __global__ __launch_bounds__(256) void dice_partial_kernel(const float* __restri
     }
 }
 
+// One wave per (image, class) term (the 4 waves take terms w, w + 4, ...): lane b sums the block
+// partials b, b + 64, ... in double, an xor-shuffle tree (fixed lane order) combines the lanes;
+// the dice / iou terms are then added in term order by thread 0 -- deterministic, and no thread
+// walks all nblk partials serially.
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 __global__ __launch_bounds__(256) void dice_finalize_kernel(const float* __restrict__ part, int N, int nblk, int ncls,
                                                             float smooth, float* __restrict__ sums,
                                                             float* __restrict__ result) {
-    double dsum = 0.0, isum = 0.0;
-    for (int idx = threadIdx.x; idx < N * ncls; idx += 256) {
-        const int n = idx / ncls, c = idx % ncls;
-        double I = 0.0, T = 0.0, P = 0.0;
-        for (int b = 0; b < nblk; ++b) {
-            const int64_t base = (((int64_t)n * nblk + b) * 3) * ncls + c;
-            I += part[base];
-            T += part[base + ncls];
-            P += part[base + 2 * ncls];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int kMaxTerms = 1024;  // terms kept in LDS for the ordered sum (N * ncls beyond: second pass)
+    __shared__ float td[kMaxTerms], ti[kMaxTerms];
+    __shared__ double acc[2];
+    if (threadIdx.x == 0) acc[0] = acc[1] = 0.0;
+    for (int base = 0; base < N * ncls; base += kMaxTerms) {
+        const int nt = N * ncls - base < kMaxTerms ? N * ncls - base : kMaxTerms;
+        for (int k = wave; k < nt; k += 4) {
+            const int idx = base + k, n = idx / ncls, c = idx % ncls;
+            double I = 0.0, T = 0.0, P = 0.0;
+            for (int b = lane; b < nblk; b += 64) {
+                const int64_t o = (((int64_t)n * nblk + b) * 3) * ncls + c;
+                I += part[o];
+                T += part[o + ncls];
+                P += part[o + 2 * ncls];
+            }
+            I = wave_sum_d(I);
+            T = wave_sum_d(T);
+            P = wave_sum_d(P);
+            if (lane == 0) {
+                const float fi = (float)I, ft = (float)T, fp = (float)P;
+                if (sums) {
+                    sums[idx * 3 + 0] = fi;
+                    sums[idx * 3 + 1] = ft;
+                    sums[idx * 3 + 2] = fp;
+                }
+                td[k] = (2.0f * fi + smooth) / (ft + fp + smooth);
+                ti[k] = (fi + smooth) / (ft + fp - fi + smooth);
+            }
         }
-        const float fi = (float)I, ft = (float)T, fp = (float)P;
-        if (sums) {
-            sums[idx * 3 + 0] = fi;
-            sums[idx * 3 + 1] = ft;
-            sums[idx * 3 + 2] = fp;
-        }
-        dsum += (double)((2.0f * fi + smooth) / (ft + fp + smooth));
-        isum += (double)((fi + smooth) / (ft + fp - fi + smooth));
-    }
-    __shared__ double rd[256], ri[256];
-    rd[threadIdx.x] = dsum;
-    ri[threadIdx.x] = isum;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            rd[threadIdx.x] += rd[threadIdx.x + s];
-            ri[threadIdx.x] += ri[threadIdx.x + s];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double d = acc[0], i = acc[1];
+            for (int k = 0; k < nt; ++k) {
+                d += (double)td[k];
+                i += (double)ti[k];
+            }
+            acc[0] = d;
+            acc[1] = i;
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
         const double cnt = (double)N * ncls;
-        const float dice = (float)(rd[0] / cnt);
+        const float dice = (float)(acc[0] / cnt);
         result[0] = 1.0f - dice;
         result[1] = dice;
-        result[2] = (float)(ri[0] / cnt);
+        result[2] = (float)(acc[1] / cnt);
     }
 }
 

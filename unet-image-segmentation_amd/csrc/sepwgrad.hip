@@ -254,15 +254,9 @@ SwPlan sw_plan(int n, int h, int w, int cin) {
     SwPlan p;
     p.tiles = n * (h / TH) * (w / TW);
     p.ncig = cin / CI;
-    // one block per CU (110-142 KB of LDS): m-slices a multiple of 8 (the XCD map).
-    // UNET_SW_BLOCKS (tuning): total blocks instead of one per CU
-    static int target = -1;
-    if (target < 0) {
-        const char* e = getenv("UNET_SW_BLOCKS");
-        target = e ? atoi(e) : 0;
-        if (target <= 0) target = resident_cus();
-    }
-    int S = (int)cdiv(target, p.ncig);
+    // one block per CU (110-142 KB of LDS): m-slices a multiple of 8 (the XCD map).  (128 / 192
+    // blocks, leaving CUs to the main stream, measured -1.7 / -0.3 % img/s.)
+    int S = (int)cdiv(resident_cus(), p.ncig);
     S = (int)cdiv(S, 8) * 8;
     p.tps = (int)cdiv(p.tiles, S);
     p.S = S;

@@ -155,17 +155,11 @@ class UNetEngine:
         # depthwise output y from the block's input view (unet_sepconv_bwd_filter), so their
         # forward never stores y
         self.recompute_y = os.environ.get("UNET_RECOMPUTE_Y", "1") != "0"
-        # ... also for the 128-output blocks of the 128 x 128 level (UNET_RECOMPUTE_Y128=1)
-        self.recompute_y128 = os.environ.get("UNET_RECOMPUTE_Y128", "0") != "0"
         # issue a y-recomputing block's fused weight gradient (one 111 KB-LDS block per CU for the
         # launch's whole length) only after the main stream has issued the NEXT block's statistics
         # finish, instead of beside its own depthwise data gradient (single-process runs only: with
         # a gradient hook the all-reduce low-water mark must not overtake it)
         self.defer_sw = os.environ.get("UNET_SW_DEFER", "1") != "0"
-        # enc1_block2's weight gradients on the main stream right after its data gradient (the side
-        # stream is still busy with the 128 x 128 level's weight gradients there; UNET_TAIL_MAIN=1)
-        self.tail_main = os.environ.get("UNET_TAIL_MAIN", "0") != "0"
-        self._tail = False
         self._pending_side = None
         self._ev = None  # created on first use (on the device)
 
@@ -271,7 +265,8 @@ class UNetEngine:
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view
             stats = training and self.use_bn
-            bb.y_recompute = training and self.recompute_y and (b.cout == 64 or self.recompute_y128) and \
+            # (64-output blocks only: the 128-output kernel measured -1.3 % img/s at the 128 x 128 level)
+            bb.y_recompute = training and self.recompute_y and b.cout == 64 and \
                 ops.sepconv_bwd_filter_supported(view, n, h, w, b.cout)
             keep_y = training and not bb.y_recompute
             ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
@@ -405,6 +400,17 @@ class UNetEngine:
         else:
             self._ev.wait(main, self.side)
 
+    def run_beside(self, fn):
+        """Run fn's launches on the side stream after the main stream's work so far (inline when
+        single-stream).  The backward ends with the main stream waiting for the side stream, so
+        the step's result includes them."""
+        if not self.overlap:
+            fn()
+            return
+        self._side_wait_main()
+        with torch.cuda.stream(self.side):
+            fn()
+
     def _flush_side(self):
         """Issue the deferred side-stream weight gradients (UNET_SW_DEFER), if any."""
         if self._pending_side is not None:
@@ -495,12 +501,9 @@ class UNetEngine:
 
         # the image block (dx0 None) has no data gradient after this: its weight gradients run
         # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
-        on_main_after = False
         if self.overlap and dx0 is not None:
             self._flush_side()
-            if self._tail and self.tail_main and self.grad_hook is None:
-                on_main_after = True
-            elif self.defer_sw and bb.y_recompute and self.grad_hook is None:
+            if self.defer_sw and bb.y_recompute and self.grad_hook is None:
                 self._pending_side = weight_grads
             else:
                 self._side_wait_main()
@@ -519,8 +522,6 @@ class UNetEngine:
                 tb.bn_slabs = S
             else:
                 ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
-        if on_main_after:
-            weight_grads()
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
     def _view_of(self, A: Acts, b: Block) -> View:
@@ -595,9 +596,7 @@ class UNetEngine:
         self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, stats_target=e4)
         for j in reversed(range(len(self.enc))):
             stage, e1, e2 = self.enc[j]
-            self._tail = j == 0
             self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da, stats_target=A.blocks[e1.name])
-            self._tail = False
             if j > 0:
                 pb = A.blocks[self.enc[j - 1][2].name]
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)

@@ -101,8 +101,9 @@ class UNetModel:
         main.wait_stream(caller)
         with torch.cuda.stream(main):
             res = self.engine.forward_train(x, y)
-            if self.mean_iou is not None:
-                self.mean_iou.update_state(y, self.engine.acts(x.shape[0]).prob)
+            if self.mean_iou is not None:  # metric only: off the critical path (the idle side stream)
+                prob = self.engine.acts(x.shape[0]).prob
+                self.engine.run_beside(lambda: self.mean_iou.update_state(y, prob))
             if self.loss_kind == L.LOSS_IOU:
                 res = res.clone()
                 res[0] = 1.0 - res[2]
