@@ -121,6 +121,21 @@ __global__ __launch_bounds__(256) void reduce_chunk_kernel(float* __restrict__ p
     }
     st4(p, make_float4((float)a0, (float)a1, (float)a2, (float)a3));
 }
+// One output (L == 1: S contiguous values, e.g. the head's bias gradient partials): 1024 threads
+// stride over the values in double, then a fixed-order LDS tree.
+__global__ __launch_bounds__(1024) void reduce_one_kernel(const float* __restrict__ part, int S, float* __restrict__ out,
+                                                          int64_t row, int64_t ld_out) {
+    double a = 0.0;
+    for (int s = threadIdx.x; s < S; s += 1024) a += (double)part[s];
+    __shared__ double red[1024];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int h = 512; h > 0; h >>= 1) {
+        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) store_out(out, 0, row, ld_out, red[0]);
+}
 // Scalar fallback for L % 4 != 0: block = 64 outputs x 16 slab groups.
 __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t L, int64_t sp,
                                                             float* __restrict__ out, int64_t row, int64_t ld_out) {
@@ -196,6 +211,8 @@ int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t
             reduce_grp4_kernel<16><<<(unsigned)cdiv(quads, 32), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
         else
             reduce_grp4_kernel<32><<<(unsigned)cdiv(quads, 16), 512, 0, stream>>>(part, S, L, sp, out, row, ld_out);
+    } else if (L == 1) {
+        reduce_one_kernel<<<1, 1024, 0, stream>>>(part, S, out, row, ld_out);
     } else {
         reduce_slabs_kernel<<<(unsigned)cdiv(L, 64), 1024, 0, stream>>>(part, S, L, sp, out, row, ld_out);
     }
