@@ -32,11 +32,6 @@ namespace {
 constexpr int RX = BK + 4;                 // halo pixel stride (floats)
 constexpr int HPIX = HHp * HWp;            // 180 halo pixels
 
-template <int S>
-struct Set {  // compile-time staging register set
-    static constexpr int value = S;
-};
-
 // tile column of the pixel that lane lo (0..31) of a wave owns (row 2w + (lo >> 4))
 __device__ __forceinline__ int rk_col(int lo) { return lo < 16 ? lo : ((lo + 14) & 15); }
 template <int BN>
@@ -90,18 +85,13 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
         else
             sp[j] = ok ? lp[j] : 0;
     }
-    // two register sets for the staging loads (set S of stage kt is kt & 1): stage kt + 3's loads
-    // are issued while stage kt + 2's are still in flight, so two stages of halo / B bytes are
-    // outstanding per block (the 256 x 256 level's launches are HBM-bound and one stage in flight
-    // per block was ~25 KB per CU, ~2.7 TB/s)
-    float4 hx[2][HR][NP];
-    float4 hsc[2], hsh[2], htap[2];
-    int hc[2] = {0, 0};
-    bool hbn[2] = {false, false};
-    auto load_halo = [&](auto S_, int k0) {
-        constexpr int S = decltype(S_)::value;
+    float4 hx[HR][NP];
+    float4 hsc, hsh, htap;
+    int hc = 0;
+    bool hbn = false;
+    auto load_halo = [&](int k0) {
         const int c = k0 + 4 * hq;
-        hc[S] = c;
+        hc = c;
         const bool cok = c < Cin;
         const float* src = g.x.src0;
         int cs = g.x.c0, ci = cok ? c : 0;
@@ -118,77 +108,71 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
                 bn = true;
             }
         }
-        hbn[S] = bn;
+        hbn = bn;
         if constexpr (MODE != UNET_VIEW_PLAIN) {
-            hsc[S] = bn ? ld4(scp + ci) : f4(1.f);
-            hsh[S] = bn ? ld4(shp + ci) : f4(0.f);
+            hsc = bn ? ld4(scp + ci) : f4(1.f);
+            hsh = bn ? ld4(shp + ci) : f4(0.f);
         }
 #pragma unroll
         for (int j = 0; j < HR; ++j) {
             const float* b = src + (sp[j] * cs + ci);
-            hx[S][j][0] = ld4(b);
+            hx[j][0] = ld4(b);
             if constexpr (NP == 4) {
                 const int rs = 2 * g.W * cs;
-                hx[S][j][1] = ld4(b + cs);
-                hx[S][j][2] = ld4(b + rs);
-                hx[S][j][3] = ld4(b + rs + cs);
+                hx[j][1] = ld4(b + cs);
+                hx[j][2] = ld4(b + rs);
+                hx[j][3] = ld4(b + rs + cs);
             }
         }
         const int tq = tid < 9 * (BK / 4) ? tid : 0;
         const int tp = tq / (BK / 4), c2 = k0 + 4 * (tq % (BK / 4));
-        htap[S] = ld4(g.dk + tp * Cin + (c2 < Cin ? c2 : 0));
+        htap = ld4(g.dk + tp * Cin + (c2 < Cin ? c2 : 0));
     };
-    auto store_halo = [&](auto S_, int buf) {
-        constexpr int S = decltype(S_)::value;
-        const bool cok = hc[S] < Cin;
+    auto store_halo = [&](int buf) {
+        const bool cok = hc < Cin;
 #pragma unroll
         for (int j = 0; j < HR; ++j) {
             const int e = tid + 256 * j;
-            float4 v = hx[S][j][0];
+            float4 v = hx[j][0];
             if constexpr (NP == 4) {
-                v = fma4(v, hsc[S], hsh[S]);
-                v = max4(v, fma4(hx[S][j][1], hsc[S], hsh[S]));
-                v = max4(v, fma4(hx[S][j][2], hsc[S], hsh[S]));
-                v = max4(v, fma4(hx[S][j][3], hsc[S], hsh[S]));
+                v = fma4(v, hsc, hsh);
+                v = max4(v, fma4(hx[j][1], hsc, hsh));
+                v = max4(v, fma4(hx[j][2], hsc, hsh));
+                v = max4(v, fma4(hx[j][3], hsc, hsh));
                 v = relu4(v);
             } else if constexpr (MODE != UNET_VIEW_PLAIN) {
-                if (hbn[S]) v = bnrelu4(v, hsc[S], hsh[S]);
+                if (hbn) v = bnrelu4(v, hsc, hsh);
             }
             if constexpr (DROP) {
-                const uint64_t i = (uint64_t)(lp[j] < 0 ? 0 : lp[j]) * C + hc[S];
+                const uint64_t i = (uint64_t)(lp[j] < 0 ? 0 : lp[j]) * C + hc;
                 v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
             }
             if (lp[j] < 0 || !cok) v = f4(0.f);
             if (e < NH) *reinterpret_cast<float4*>(&Xs(buf)[(e >> 2) * RX + 4 * (e & 3)]) = v;
         }
         if (tid < 9 * (BK / 4)) {
-            const int c2 = hc[S] - 4 * hq + 4 * (tid % (BK / 4));
-            *reinterpret_cast<float4*>(&Ks(buf)[4 * tid]) = c2 < Cin ? htap[S] : f4(0.f);
+            const int c2 = hc - 4 * hq + 4 * (tid % (BK / 4));
+            *reinterpret_cast<float4*>(&Ks(buf)[4 * tid]) = c2 < Cin ? htap : f4(0.f);
         }
     };
     // ---- B staging: thread loads float4 (k-row, n-quad) of the n-contiguous weights
-    float4 rb[2][BQ];
-    bool bok[2][BQ];
+    float4 rb[BQ];
+    bool bok[BQ];
     constexpr int NQ = BN / 4;
     const int bq_k = tid / NQ, bq_n = tid % NQ;
-    auto load_b = [&](auto S_, int k0) {
-        constexpr int S = decltype(S_)::value;
+    auto load_b = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const int kk = k0 + bq_k + (256 / NQ) * r, nn = n0 + 4 * bq_n;
-            bok[S][r] = kk < Cin && nn < g.Cout;
-            rb[S][r] = ld4(g.pk + (bok[S][r] ? (int64_t)kk * g.Cout + nn : 0));
+            bok[r] = kk < Cin && nn < g.Cout;
+            rb[r] = ld4(g.pk + (bok[r] ? (int64_t)kk * g.Cout + nn : 0));
         }
     };
-    auto store_b = [&](auto S_, int buf) {
-        constexpr int S = decltype(S_)::value;
+    auto store_b = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r)
-            *reinterpret_cast<float4*>(&Bs(buf)[(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) =
-                bok[S][r] ? rb[S][r] : f4(0.f);
+            *reinterpret_cast<float4*>(&Bs(buf)[(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
     };
-    const Set<0> s0;
-    const Set<1> s1;
 
     // ---- this lane's pixel: tile row 2 wave + (lo >> 4), column rk_col(lo)
     const int pr = 2 * wave + (lo >> 4), pc = rk_col(lo);
@@ -249,30 +233,26 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
 
     // Three-slot ring (halo, taps, B): stage kt computes from slot kt % 3 and already evaluates
     // the depthwise of stage kt+1's first k-group from slot (kt+1) % 3 (staged one stage ahead),
-    // while the global loads of stages kt+2 (register set kt & 1) and kt+3 (the other set) are in
-    // flight; stage kt+2's are written into slot (kt+2) % 3, last read during stage kt-1.  One
-    // barrier per stage.
+    // while the global loads of stage kt+2 are in flight; they are written into slot (kt+2) % 3,
+    // last read during stage kt-1.  One barrier per stage.
     const int nk = (Cin + BK - 1) / BK;
-    load_halo(s0, 0);
-    load_b(s0, 0);
-    load_halo(s1, BK);
-    load_b(s1, BK);
-    store_halo(s0, 0);
-    store_b(s0, 0);
-    load_halo(s0, 2 * BK);
-    load_b(s0, 2 * BK);
-    store_halo(s1, 1);
-    store_b(s1, 1);
+    load_halo(0);
+    load_b(0);
+    store_halo(0);
+    store_b(0);
+    load_halo(BK);
+    load_b(BK);
+    store_halo(1);
+    store_b(1);
     __syncthreads();
     float4 a = dw(0, 0);
-    // one stage; P: the set holding stage kt + 2 (loaded one stage earlier), Q: the set that loads
-    // stage kt + 3.  Loads past the last stage come from clamped addresses and are never stored:
-    // the body stays branch-free around the loads; the last stage's look-ahead depthwise reads a
-    // stale (valid) slot and is discarded
-    auto stage = [&](auto P, auto Q, int kt) {
+    for (int kt = 0; kt < nk; ++kt) {
         const int cb = kt % 3, nb = (kt + 1) % 3, wb = (kt + 2) % 3;
-        load_halo(Q, (kt + 3) * BK);
-        load_b(Q, (kt + 3) * BK);
+        // loads past the last stage come from clamped addresses and are never stored: the loop
+        // body stays branch-free around the loads; the last stage's look-ahead depthwise reads a
+        // stale (valid) slot and is discarded
+        load_halo((kt + 2) * BK);
+        load_b((kt + 2) * BK);
         const float4 a1 = mfma_dw(a, cb, 0, cb, 1);
         const float4 a0 = mfma_dw(a1, cb, 1, nb, 0);
         if constexpr (WRITE_Y) {  // y (depthwise output) for the pointwise weight gradient
@@ -284,14 +264,10 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
         }
         a = a0;
         if (kt + 2 < nk) {
-            store_halo(P, wb);
-            store_b(P, wb);
+            store_halo(wb);
+            store_b(wb);
         }
         __syncthreads();
-    };
-    for (int kt = 0; kt < nk; kt += 2) {
-        stage(s0, s1, kt);
-        if (kt + 1 < nk) stage(s1, s0, kt + 1);
     }
 
     // ---- epilogue (the loop ended on a barrier: the ring is free).  Accumulator row
