@@ -88,3 +88,37 @@ def test_engine_refuses_without_device():
     from unet_amd.engine import UNetEngine
     with pytest.raises(RuntimeError, match="no CPU execution path"):
         UNetEngine((32, 32, 3))
+
+
+from unet_amd import _lib  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _lib.load()
+
+
+# argument validation of every entry point: null pointers and zero sizes are refused (or, for the
+# size / support queries, answered with 0) before any device call -- runs without a GPU
+_QUERIES = ("_workspace", "_size", "_slabs", "_supported", "unet_abi_version", "unet_last_error",
+            "unet_event_destroy", "unet_sepconv_set_schedule")
+
+
+@pytest.mark.parametrize("name", sorted(_lib.SIGNATURES))
+def test_entry_point_rejects_null_arguments(lib, name):
+    res, args = _lib.SIGNATURES[name]
+    f = getattr(lib, name)
+    f.restype, f.argtypes = res, args
+    vals = []
+    for a in args:
+        if a in (ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_uint64):
+            vals.append(0)
+        elif a is ctypes.c_float:
+            vals.append(0.0)
+        else:
+            vals.append(None)
+    r = f(*vals)
+    if name.endswith(_QUERIES) or name in _QUERIES:
+        return
+    assert r != 0, f"{name} accepted null / zero arguments"
+    assert lib.unet_last_error(), f"{name} refused without an error message"
