@@ -160,12 +160,6 @@ class UNetEngine:
         # finish, instead of beside its own depthwise data gradient (single-process runs only: with
         # a gradient hook the all-reduce low-water mark must not overtake it)
         self.defer_sw = os.environ.get("UNET_SW_DEFER", "1") != "0"
-        # the 128 x 128 level's pooled block (enc2_block1): its depthwise filter gradient on the main
-        # stream after the image block, instead of at the end of the side stream's backlog (the side
-        # stream is the step's critical path there; UNET_TAIL_DWF=1)
-        self.tail_dwf = os.environ.get("UNET_TAIL_DWF", "0") != "0"
-        self._tail_dwf_block = False
-        self._main_tail = []
         self._pending_side = None
         self._ev = None  # created on first use (on the device)
 
@@ -493,17 +487,12 @@ class UNetEngine:
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gdk, gpk = self._gwts(b)
 
-        tail_dwf = self._tail_dwf_block and self.tail_dwf and self.overlap and self.grad_hook is None
-
         def weight_grads():
             if bb.y_recompute:  # both kernels' gradients in one pass, y recomputed from view_in
                 ops.sepconv_bwd_filter(view_in, n, h, w, dk, dy, dz, b.cout, gdk, gpk)
                 return
             if not img_wg:  # (the image block's was accumulated by its data-gradient pass)
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            if tail_dwf:
-                self._main_tail.append(lambda: ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk))
-                return
             ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 ops.copy_strided(gpk, 1, b.wcin * b.cout, b.cin * b.cout,
@@ -610,15 +599,10 @@ class UNetEngine:
             self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da, stats_target=A.blocks[e1.name])
             if j > 0:
                 pb = A.blocks[self.enc[j - 1][2].name]
-                self._tail_dwf_block = j == 1
                 self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
-                self._tail_dwf_block = False
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
         self._flush_side()
-        for fn in self._main_tail:
-            fn()
-        self._main_tail = []
         if self.overlap:
             self._main_wait_side()
 
