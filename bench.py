@@ -164,6 +164,8 @@ def workload_config(args):
         return "configs[3] (per-GPU shape)"
     if args.size == 256 and args.num_classes == 21 and args.batch == 8:
         return "configs[4] (per-GPU shape, batch 32 over 4 GPUs)"
+    if args.size == 256 and args.num_classes == 21 and args.batch == 32:
+        return "configs[4] (its whole batch of 32 on one GPU)"
     return "custom"
 
 
