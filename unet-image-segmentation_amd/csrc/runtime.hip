@@ -227,6 +227,14 @@ namespace {
 __global__ __launch_bounds__(256) void copy_strided_kernel(const float* __restrict__ src, int64_t rows, int cols,
                                                            int64_t src_ld, float* __restrict__ dst, int64_t dst_ld) {
     const int64_t n = rows * cols;
+    if (n < (int64_t(1) << 31)) {  // 32-bit index math (a 64-bit division per element doubled the launch)
+        const unsigned uc = (unsigned)cols;
+        for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < (unsigned)n; i += gridDim.x * 256u) {
+            const unsigned r = i / uc, c = i - r * uc;
+            dst[(int64_t)r * dst_ld + c] = src[(int64_t)r * src_ld + c];
+        }
+        return;
+    }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const int64_t r = i / cols, c = i - r * cols;
         dst[r * dst_ld + c] = src[r * src_ld + c];
