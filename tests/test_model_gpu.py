@@ -195,6 +195,30 @@ def test_determinism_bitwise():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+def test_stream_schedules_bitwise_equal():
+    """The schedule only orders launches: single-stream, two-stream with the weight gradients issued
+    beside their data gradient, and two-stream with the fused 256x256-level weight gradient deferred
+    past the next statistics launch give the same bits after two steps (with the MeanIoU update on
+    the side stream).  128 x 128 input, batch 2: enc1's blocks take the fused y-recompute route."""
+    from unet_amd.model import UNetModel
+    from unet_amd.metrics import MeanIoU
+    rng = np.random.default_rng(11)
+    x, y = _data(rng, 2, 128, 128, 1)
+    outs = []
+    for overlap, defer in ((False, False), (True, False), (True, True)):
+        m = UNetModel((128, 128, 3), 1, seed=7)
+        m.engine.overlap, m.engine.defer_sw = overlap, defer
+        miou = MeanIoU(2, threshold=0.5)
+        m.compile(None, "dice_loss", [miou])
+        m.train_step(x, y)
+        m.train_step(x, y)
+        torch.cuda.synchronize()
+        outs.append((m.engine.params.cpu().clone(), m.engine.stats.cpu().clone(), miou.confusion_matrix()))
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
+        assert (outs[0][2] == o[2]).all()
+
+
 def test_full_size_train_steps_cfg2():
     """configs[1] shape (256x256x3, batch 16): loss decreases on a fixed batch, no NaNs, and
     size-independent properties hold (probabilities in [0,1], dice = 1 - loss)."""
