@@ -240,6 +240,20 @@ __global__ __launch_bounds__(256) void copy_strided_kernel(const float* __restri
         dst[r * dst_ld + c] = src[r * src_ld + c];
     }
 }
+// rows of <= 4 floats into 16-B aligned rows of 4 (the image's channel padding): one float4 store
+// per row, the columns past `cols` kept as they are
+__global__ __launch_bounds__(256) void copy_rows4_kernel(const float* __restrict__ src, int64_t rows, int cols,
+                                                         int64_t src_ld, float4* __restrict__ dst) {
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
+        float4 v = dst[r];
+        const float* p = src + r * src_ld;
+        v.x = p[0];
+        if (cols > 1) v.y = p[1];
+        if (cols > 2) v.z = p[2];
+        if (cols > 3) v.w = p[3];
+        dst[r] = v;
+    }
+}
 }  // namespace
 }  // namespace unet
 
@@ -249,6 +263,13 @@ extern "C" int unet_copy_strided(const float* src, int64_t rows, int cols, int64
     UNET_CHECK_ARG(rows >= 0 && cols >= 0 && src_ld >= cols && dst_ld >= cols, "unet_copy_strided: bad sizes");
     const int64_t n = rows * cols;
     if (n == 0) return 0;
+    if (cols <= 4 && dst_ld == 4 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int64_t blocks = (rows + 255) / 256 < 4096 ? (rows + 255) / 256 : 4096;
+        unet::copy_rows4_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
+            src, rows, cols, src_ld, reinterpret_cast<float4*>(dst));
+        UNET_CHECK_LAUNCH("unet_copy_strided");
+        return 0;
+    }
     const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
     unet::copy_strided_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(src, rows, cols, src_ld,
                                                                                               dst, dst_ld);
