@@ -146,7 +146,8 @@ def pmc_traffic(op):
     """HBM bytes per launch of `op` from the newest committed PMC summary (profiles/*_traffic.json,
     written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench)."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+    files = glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))
+    for f in sorted(files, key=lambda f: (os.path.getmtime(f), f), reverse=True):  # newest first
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
