@@ -583,13 +583,8 @@ __global__ __launch_bounds__(256, 2) void dw_tile_bwd_fused(DView v, int N, int 
 }
 
 int qt_for(int C) {
-    static int wide = -1;  // channel quads per tile when C % 64 == 0 (UNET_DW_QT: tuning, 16 or 8)
-    if (wide < 0) {
-        const char* e = getenv("UNET_DW_QT");
-        wide = e && atoi(e) == 8 ? 8 : 16;
-    }
     if (C % 4) return 0;
-    if (C % 64 == 0) return wide;
+    if (C % 64 == 0) return 16;  // (8 quads x 32 columns measured -0.6 % img/s, round 2)
     const int q = C / 4;
     return (q == 1 || q == 2 || q == 4 || q == 8) ? q : 0;
 }
