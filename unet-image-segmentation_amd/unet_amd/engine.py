@@ -142,7 +142,6 @@ class UNetEngine:
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
         # profiles/r1i_sepconv_bn_sweep.log); "always" / "never" force the choice (tests).
         self.fuse_sepconv = "auto"
-        self.fuse_min_hw = int(os.environ.get("UNET_FUSE_MIN_HW", 64 * 64))  # "auto": levels of >= this many pixels
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
         # BN-backward statistics of a block emitted by the launch that completes its da (the next
@@ -261,7 +260,7 @@ class UNetEngine:
         bb = A.blocks[b.name]
         gamma, beta, mm, mv = self._bn(b.name)
         dk, pk = self._wts(b)
-        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= self.fuse_min_hw)
+        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= 64 * 64)
         if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view
