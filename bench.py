@@ -22,6 +22,8 @@ import argparse
 import json
 import os
 import sys
+
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # as unet_amd/__init__.py: before HIP initialises
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

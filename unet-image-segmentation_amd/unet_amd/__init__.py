@@ -1,6 +1,13 @@
 """unet_amd: MI355X-native engine for the separable-conv U-Net hot path of
 planck-epoch/unet-image-segmentation (HIP kernels for gfx950 behind a C-ABI,
 include/unet_hip.h; PyTorch-ROCm only for device memory, streams and RCCL)."""
+import os as _os
+
+# Kernel arguments in device memory: the step is ~210 dependent launches, and reading each launch's
+# arguments from host memory lengthened every kernel boundary (step A/B on MI355X: 1390 vs 1368
+# img/s, profiles/r2x_ab.log).  Read by the HIP runtime when it initialises, so it is set here,
+# before any device call; an explicit setting in the environment wins.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 from ._lib import UnetHipError, load as load_library  # noqa: F401
 from .params import FILTERS, unet_variables  # noqa: F401
 
