@@ -206,6 +206,21 @@ def cpu_baseline(size, ncls, batch):
                       f"{r['threads']} threads"}
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: run this same command as N torchrun ranks (one
+    process per GPU) in a CHILD process and relay its exit code.  Called before anything touches
+    the GPU (no torch / HIP initialisation in this parent), so no process that owns a device
+    context is replaced."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,6 +234,10 @@ def main():
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -229,6 +248,10 @@ def main():
     from unet_amd.optim import AdamW
 
     rank, world, local = init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if os.environ.get("UNET_DP_ONE_DEVICE") != "1" and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPU(s)")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     model = UNetModel((args.size, args.size, 3), args.num_classes, dropout_rate=0.2, device=device)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 7
+#define UNET_ABI_VERSION 8
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -126,20 +126,6 @@ int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w,
                                     const float* rstd, float* bn_partials,
                                     unet_stream_t stream);
 
-/* Data and filter gradient in one pass over dy (dy read once): dx0/dx1 as
- * unet_dwconv3x3_bwd_data (dx0 may be NULL for PLAIN/BNRELU views: filter only),
- * d_dw_kernel as unet_dwconv3x3_bwd_filter (workspace: _bwd_workspace), and with
- * bn_partials != NULL (BNRELU / POOL_BNRELU views) the view block's
- * BatchNorm-backward partials as unet_dwconv3x3_bwd_data_bnstats, over
- * S = unet_dwconv3x3_bwd_slabs(...) slabs (0: no such path for this shape).  */
-int unet_dwconv3x3_bwd_slabs(const unet_view* x, int n, int h, int w);
-size_t unet_dwconv3x3_bwd_workspace(int n, int h, int w, int c);
-int unet_dwconv3x3_bwd(const unet_view* x, int n, int h, int w,
-                       const float* dw_kernel, const float* dy, float* dx0,
-                       float* dx1, float* d_dw_kernel, const float* mean,
-                       const float* rstd, float* bn_partials, void* ws,
-                       size_t ws_bytes, unet_stream_t stream);
-
 size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c);
 /* d_dw_kernel (3,3,C,1) = sum over pixels of x(shifted) * dy (overwrites). */
 int unet_dwconv3x3_bwd_filter(const unet_view* x, int n, int h, int w,
@@ -163,16 +149,6 @@ size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout);
 int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
                               int cin, int cout, float* d_pw_kernel,
                               void* ws, size_t ws_bytes, unet_stream_t stream);
-/* Same gradient with dz formed on load from (da, z) and the coefficients of
- * unet_bn_relu_bwd_stats (no dropout on the block output), so the data-gradient
- * GEMM need not store dz (dz = NULL there).  Workspace as unet_pointwise_bwd_filter. */
-int unet_pointwise_bwd_filter_bnrelu(const float* y, const float* da,
-                                     const float* z, int64_t m, int cin, int cout,
-                                     const float* scale, const float* shift,
-                                     const float* coef, float* d_pw_kernel,
-                                     void* ws, size_t ws_bytes,
-                                     unet_stream_t stream);
-
 /* Fused SeparableConv2D: depthwise 3x3 of the view -> pointwise 1x1 (+ BatchNorm partials as
  * unet_pointwise_fwd), the depthwise result never leaving the chip except as the optional `y`
  * (needed by the pointwise weight gradient in training; NULL for inference).  Supported when

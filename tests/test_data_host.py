@@ -115,3 +115,41 @@ def test_prefetcher_finite_source_ends():
     items = [(np.ones((1, 2, 2, 3)) * i, np.zeros((1, 2, 2, 1))) for i in range(4)]
     out = list(Prefetcher(items, device="cpu", depth=1))
     assert [float(o[0][0, 0, 0, 0]) for o in out] == [0, 1, 2, 3]
+
+
+def test_prefetcher_limit_keeps_single_pass_generator_batches():
+    """A shared one-shot generator loses no batches to read-ahead (evaluate on a
+    Keras-style flow): with limit=k the producer pulls exactly k batches per iteration."""
+    def gen():
+        i = 0
+        while True:
+            yield np.full((1, 2, 2, 3), i, np.float32), np.zeros((1, 2, 2, 1), np.float32)
+            i += 1
+    g = gen()
+    for epoch in range(3):
+        it = iter(Prefetcher(g, device="cpu", depth=4, limit=2))
+        got = [float(next(it)[0][0, 0, 0, 0]) for _ in range(2)]
+        assert got == [2 * epoch, 2 * epoch + 1]
+        with pytest.raises(StopIteration):
+            next(it)
+
+
+def test_prefetcher_restart_isolates_iterations():
+    """Re-iterating one Prefetcher: the previous producer is joined before a new one starts, so a
+    late producer can never push batches of the old iteration into the new queue."""
+    import time
+
+    class Slow:
+        def __iter__(self):
+            i = 0
+            while True:
+                time.sleep(0.01)
+                yield np.full((1, 2, 2, 3), i, np.float32), np.zeros((1, 2, 2, 1), np.float32)
+                i += 1
+    pf = Prefetcher(Slow(), device="cpu", depth=2)
+    for _ in range(4):
+        it = iter(pf)
+        first = [float(next(it)[0][0, 0, 0, 0]) for _ in range(3)]
+        assert first == [0.0, 1.0, 2.0]  # every iteration starts a fresh pass of the source
+    pf.close()
+    assert pf._thread is None

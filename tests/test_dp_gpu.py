@@ -37,3 +37,23 @@ def test_dp_two_ranks_equal_weighted_single_process(global_batch):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "identical across ranks: True" in r.stdout
     assert r.stdout.count("equal to expected: True") == 2, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` (the driver's command shape, no launcher environment) runs two
+    ranks: the parent starts torch.distributed.run as a child before touching the GPU, and the
+    JSON line reports both GPUs and the global batch."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if torch.cuda.device_count() < 2:
+        env["UNET_DP_ONE_DEVICE"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-roofline", "--encoder-batch", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 32, out
+    assert out["config"]["parallelism"] == "dp2"

@@ -35,6 +35,15 @@ inline hipStream_t as_stream(unet_stream_t s) { return reinterpret_cast<hipStrea
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Tuning knobs read from the environment exist only in the lab build (`make lab` ->
+// libunet_hip_lab.so, -DUNET_LAB_BUILD, loaded by the tools through UNET_HIP_LIB).  The product
+// library reads no environment: every call's behaviour is a function of its arguments.
+#ifdef UNET_LAB_BUILD
+int lab_knob(const char* name, int dflt);  // runtime.hip
+#else
+inline int lab_knob(const char*, int dflt) { return dflt; }
+#endif
+
 // -------------------------------------------------------------- vectors ----
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));

@@ -385,10 +385,6 @@ int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H,
                               const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
                               hipStream_t st);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
-int dw_tiled_fused_blocks(int N, int H, int W, int C);
-int dw_tiled_bwd_fused(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
-                       float* dx0, float* dx1, float* fpart, const float* mu, const float* rs, float* bnpart,
-                       hipStream_t st);
 
 static int check_dims(const unet_view* x, int n, int h, int w, const char* op) {
     UNET_CHECK_ARG(n > 0 && h > 0 && w > 0, "%s: bad shape n=%d h=%d w=%d", op, n, h, w);
@@ -468,43 +464,6 @@ extern "C" int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h,
     const DView v = make_dview(*x);
     return dw_tiled_bwd_data_bnstats(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
                                      as_stream(stream));
-}
-
-extern "C" int unet_dwconv3x3_bwd_slabs(const unet_view* x, int n, int h, int w) {
-    if (!x || n <= 0 || h <= 0 || w <= 0 || !view_vec(x)) return 0;
-    const int C = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
-    if (!dw_tiled_ok(C)) return 0;
-    return dw_tiled_fused_blocks(n, h, w, C);
-}
-
-extern "C" size_t unet_dwconv3x3_bwd_workspace(int n, int h, int w, int c) {
-    if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || !dw_tiled_ok(c)) return 0;
-    return align_up((size_t)dw_tiled_fused_blocks(n, h, w, c) * 9 * c * sizeof(float), 256);
-}
-
-extern "C" int unet_dwconv3x3_bwd(const unet_view* x, int n, int h, int w, const float* dw_kernel, const float* dy,
-                                  float* dx0, float* dx1, float* d_dw_kernel, const float* mean, const float* rstd,
-                                  float* bn_partials, void* ws, size_t ws_bytes, unet_stream_t stream) {
-    const char* op = "unet_dwconv3x3_bwd";
-    if (check_view(x, op) || check_dims(x, n, h, w, op)) return -1;
-    UNET_CHECK_ARG(dw_kernel && dy && d_dw_kernel, "%s: null pointer", op);
-    UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU || dx0, "%s: view needs dx0", op);
-    UNET_CHECK_ARG(x->mode != UNET_VIEW_CONCAT || dx1, "%s: CONCAT view needs dx1", op);
-    UNET_CHECK_ARG(!bn_partials || x->mode == UNET_VIEW_BNRELU || x->mode == UNET_VIEW_POOL_BNRELU,
-                   "%s: bn_partials need a BNRELU or POOL_BNRELU view", op);
-    UNET_CHECK_ARG(!bn_partials || dx0, "%s: bn_partials need dx0", op);
-    UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "%s: mean and rstd go together", op);
-    const int S = unet_dwconv3x3_bwd_slabs(x, n, h, w);
-    UNET_CHECK_ARG(S > 0, "%s: needs channels %% 4 == 0 (tiled path)", op);
-    const DView v = make_dview(*x);
-    const size_t need = unet_dwconv3x3_bwd_workspace(n, h, w, v.C);
-    UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
-    float* part = static_cast<float*>(ws);
-    hipStream_t st = as_stream(stream);
-    int rc = dw_tiled_bwd_fused(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, dx1, part, mean, rstd,
-                                bn_partials, st);
-    if (rc) return rc;
-    return reduce_slabs(part, S, (int64_t)9 * v.C, d_dw_kernel, (int64_t)9 * v.C, (int64_t)9 * v.C, st);
 }
 
 extern "C" size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c) {

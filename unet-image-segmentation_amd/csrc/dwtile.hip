@@ -22,10 +22,6 @@ int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H,
                               const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
                               hipStream_t st);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
-int dw_tiled_fused_blocks(int N, int H, int W, int C);
-int dw_tiled_bwd_fused(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
-                       float* dx0, float* dx1, float* fpart, const float* mu, const float* rs, float* bnpart,
-                       hipStream_t st);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
 bool dw_tiled_ok(int C);
@@ -384,204 +380,6 @@ __global__ __launch_bounds__(256, 2) void dw_tile_bwd_filter(DView v, int N, int
     }
 }
 
-// Data + filter gradient in one pass over dy (persistent over tiles, one LDS halo buffer):
-// per tile, (1) stage the dy halo, (2) evaluate dx with the flipped taps as dw_tile_bwd_data does,
-// keeping this lane's 8 interior dy values in registers, route dx through the view (and emit the
-// view block's BN-backward partials when STATS), (3) stage the input-view halo into the same LDS
-// buffer and (4) accumulate the 9 filter taps from it and the registered dy.  dy is read once
-// instead of twice; the filter partial and the STATS partial are per block (fixed order).
-template <int MODE, bool DROP, int QT, bool STATS>
-__global__ __launch_bounds__(256, 2) void dw_tile_bwd_fused(DView v, int N, int H, int W, int tiles_w, int tiles_h,
-                                                         const float* __restrict__ K, const float* __restrict__ dY,
-                                                         float* __restrict__ dx0, float* __restrict__ dx1,
-                                                         float* __restrict__ fpart, const float* __restrict__ mu,
-                                                         const float* __restrict__ rs, float* __restrict__ bnpart) {
-    using G = Geom<QT>;
-    __shared__ float4 T[G::NE];
-    const int cbase = blockIdx.y * 4 * QT;
-    const int C = v.C;
-    const int q = threadIdx.x % QT, col = threadIdx.x / QT;
-    const int c = cbase + 4 * q;
-    int n, h0, w0;
-    tile_coords(blockIdx.x, tiles_w, tiles_h, G::TW, n, h0, w0);
-    const int w = w0 + col;
-    // (1) dy halo -> LDS
-    {
-        DView dv{};
-        dv.src0 = dY;
-        dv.c0 = C;
-        dv.C = C;
-        stage<UNET_VIEW_PLAIN, false, QT>(T, dv, n, h0, w0, H, W, cbase);
-    }
-    float4 s1 = f4(0.f), s2 = f4(0.f);
-    float4 gy[TH];  // interior dy of this lane's column (zero outside the image)
-    __syncthreads();
-    // (2) dx with the flipped taps, routed / stored through the view (+ STATS sums)
-    {
-        float4 smu = f4(0.f), srs = f4(0.f);
-        if constexpr (STATS) {
-            if (mu) {
-                smu = ld4(mu + c);
-                srs = ld4(rs + c);
-            }
-        }
-        float4 kf[9];  // flipped kernel: dx(h,w) = sum dy(h-i+1, w-j+1) k[i][j]
-#pragma unroll
-        for (int t = 0; t < 9; ++t) kf[t] = ld4(K + (8 - t) * C + c);
-        float4 a[3][3];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) a[i][j] = T[(i * G::HWp + col + j) * QT + q];
-#pragma unroll
-        for (int r = 0; r < TH; ++r) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
-            gy[r] = a[1][1];
-            float4 acc = f4(0.f);
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) acc = fma4(a[i][j], kf[i * 3 + j], acc);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                a[0][j] = a[1][j];
-                a[1][j] = a[2][j];
-            }
-            const int h = h0 + r;
-            if (w >= W || h >= H) continue;
-            const int p = (n * H + h) * W + w;
-            if constexpr (DROP) {
-                const uint64_t li = (uint64_t)p * C + c;
-                acc = mul4(acc, drop_mult4(v.seed, li, v.rate, v.inv_keep));
-            }
-            if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
-                if (dx0) st4(dx0 + (int64_t)p * C + c, acc);
-                if constexpr (STATS && MODE == UNET_VIEW_BNRELU) {
-                    const float4 zr = ld4(v.src0 + (int64_t)p * C + c);
-                    const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
-                    const float4 gm = make_float4(fmaf(zr.x, sc.x, sh.x) > 0.f ? acc.x : 0.f,
-                                                  fmaf(zr.y, sc.y, sh.y) > 0.f ? acc.y : 0.f,
-                                                  fmaf(zr.z, sc.z, sh.z) > 0.f ? acc.z : 0.f,
-                                                  fmaf(zr.w, sc.w, sh.w) > 0.f ? acc.w : 0.f);
-                    s1 = add4(s1, gm);
-                    const float4 xh = make_float4((zr.x - smu.x) * srs.x, (zr.y - smu.y) * srs.y,
-                                                  (zr.z - smu.z) * srs.z, (zr.w - smu.w) * srs.w);
-                    s2 = fma4(gm, xh, s2);
-                }
-            } else if constexpr (MODE == UNET_VIEW_CONCAT) {
-                if (c < v.c0)
-                    st4(dx0 + (int64_t)p * v.c0 + c, acc);
-                else
-                    st4(dx1 + (int64_t)p * v.c1 + (c - v.c0), acc);
-            } else {  // POOL_BNRELU: gradient to the first max of the 2x2 window, accumulated
-                const int W2 = 2 * W;
-                const int64_t b = ((int64_t)(n * 2 * H + 2 * h) * W2 + 2 * w) * v.c0 + c;
-                const int64_t off[4] = {0, v.c0, (int64_t)W2 * v.c0, (int64_t)W2 * v.c0 + v.c0};
-                const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
-                float4 zr[4], xv[4], g[4];
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    zr[qq] = ld4(v.src0 + b + off[qq]);
-                    xv[qq] = bnrelu4(zr[qq], sc, sh);
-                    g[qq] = ld4(dx0 + b + off[qq]);
-                }
-#define UNET_ROUTE(comp)                                                   \
-    {                                                                      \
-        float best = xv[0].comp;                                           \
-        int arg = 0;                                                       \
-        if (xv[1].comp > best) { best = xv[1].comp; arg = 1; }             \
-        if (xv[2].comp > best) { best = xv[2].comp; arg = 2; }             \
-        if (xv[3].comp > best) { best = xv[3].comp; arg = 3; }             \
-        g[0].comp += arg == 0 ? acc.comp : 0.f;                            \
-        g[1].comp += arg == 1 ? acc.comp : 0.f;                            \
-        g[2].comp += arg == 2 ? acc.comp : 0.f;                            \
-        g[3].comp += arg == 3 ? acc.comp : 0.f;                            \
-    }
-                UNET_ROUTE(x)
-                UNET_ROUTE(y)
-                UNET_ROUTE(z)
-                UNET_ROUTE(w)
-#undef UNET_ROUTE
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq) st4(dx0 + b + off[qq], g[qq]);
-                if constexpr (STATS) {
-#pragma unroll
-                    for (int qq = 0; qq < 4; ++qq) {
-                        const float4 gm = make_float4(xv[qq].x > 0.f ? g[qq].x : 0.f, xv[qq].y > 0.f ? g[qq].y : 0.f,
-                                                      xv[qq].z > 0.f ? g[qq].z : 0.f, xv[qq].w > 0.f ? g[qq].w : 0.f);
-                        s1 = add4(s1, gm);
-                        const float4 xh = make_float4((zr[qq].x - smu.x) * srs.x, (zr[qq].y - smu.y) * srs.y,
-                                                      (zr[qq].z - smu.z) * srs.z, (zr[qq].w - smu.w) * srs.w);
-                        s2 = fma4(gm, xh, s2);
-                    }
-                }
-            }
-        }
-    }
-    // (3) input-view halo into the same buffer (loads in batches of 4 to bound registers)
-    __syncthreads();
-    stage<MODE, DROP, QT, 4>(T, v, n, h0, w0, H, W, cbase);
-    __syncthreads();
-    // (4) filter taps of this tile from the x halo and the registered dy
-    float4 facc[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) facc[t] = f4(0.f);
-    {
-        float4 a[3][3];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) a[i][j] = T[(i * G::HWp + col + j) * QT + q];
-#pragma unroll
-        for (int r = 0; r < TH; ++r) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) a[2][j] = T[((r + 2) * G::HWp + col + j) * QT + q];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) facc[i * 3 + j] = fma4(a[i][j], gy[r], facc[i * 3 + j]);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                a[0][j] = a[1][j];
-                a[1][j] = a[2][j];
-            }
-        }
-    }
-    // fixed-order reductions over the TW column lanes of each channel quad -> per-tile slabs
-    float* out = fpart + (int64_t)blockIdx.x * 9 * C;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        __syncthreads();
-        T[threadIdx.x] = facc[t];
-        __syncthreads();
-        if (col == 0) {
-            float4 sacc = T[q];
-            for (int cl = 1; cl < G::TW; ++cl) sacc = add4(sacc, T[cl * QT + q]);
-            st4(out + t * C + c, sacc);
-        }
-    }
-    if constexpr (STATS) {
-        float* bo = bnpart + (int64_t)blockIdx.x * 2 * C;
-        __syncthreads();
-        T[threadIdx.x] = s1;
-        __syncthreads();
-        if (col == 0) {
-            float4 t4 = T[q];
-            for (int cl = 1; cl < G::TW; ++cl) t4 = add4(t4, T[cl * QT + q]);
-            st4(bo + c, t4);
-        }
-        __syncthreads();
-        T[threadIdx.x] = s2;
-        __syncthreads();
-        if (col == 0) {
-            float4 t4 = T[q];
-            for (int cl = 1; cl < G::TW; ++cl) t4 = add4(t4, T[cl * QT + q]);
-            st4(bo + C + c, t4);
-        }
-    }
-}
-
 int qt_for(int C) {
     if (C % 4) return 0;
     if (C % 64 == 0) return 16;  // (8 quads x 32 columns measured -0.6 % img/s, round 2)
@@ -603,12 +401,8 @@ TilePlan tile_plan(int N, int H, int W, int C) {
     return p;
 }
 int filter_blocks(const TilePlan& p) {
-    static int target = -1;  // persistent blocks over all channel chunks (UNET_DWF_BLOCKS: tuning)
-    if (target < 0) {
-        const char* e = getenv("UNET_DWF_BLOCKS");
-        target = e ? atoi(e) : 1024;
-        if (target < 1) target = 1024;
-    }
+    int target = lab_knob("UNET_DWF_BLOCKS", 1024);  // persistent blocks over all channel chunks
+    if (target < 1) target = 1024;
     int g = (int)cdiv(target, p.chunks);
     if (g > p.ntiles) g = p.ntiles;
     if (g < 1) g = 1;
@@ -696,54 +490,6 @@ int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H,
 }
 
 size_t dw_tiled_ntiles(int N, int H, int W, int C) { return (size_t)tile_plan(N, H, W, C).ntiles; }
-
-// blocks (per channel chunk) of the fused data + filter gradient: its filter / STATS slab count.
-// One tile per block (measured: a persistent 1024-block grid exposes the two dependent halo
-// loads of every tile; 3 resident blocks per CU overlap them instead).
-int dw_tiled_fused_blocks(int N, int H, int W, int C) { return tile_plan(N, H, W, C).ntiles; }
-
-int dw_tiled_bwd_fused(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
-                       float* dx0, float* dx1, float* fpart, const float* mu, const float* rs, float* bnpart,
-                       hipStream_t st) {
-    TilePlan p = tile_plan(N, H, W, v.C);
-    const int G = p.ntiles;
-    dim3 grid((unsigned)G, (unsigned)p.chunks);
-    const bool stats = bnpart != nullptr;
-#define UNET_FUSED(MODE, D, Q)                                                                                  \
-    do {                                                                                                        \
-        if (stats)                                                                                              \
-            dw_tile_bwd_fused<MODE, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, K, dY,    \
-                                                                       dx0, dx1, fpart, mu, rs, bnpart);        \
-        else                                                                                                    \
-            dw_tile_bwd_fused<MODE, D, Q, false><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, K, dY,   \
-                                                                        dx0, dx1, fpart, mu, rs, bnpart);       \
-    } while (0)
-#define UNET_FUSED_QT(MODE, D)                    \
-    switch (p.qt) {                               \
-        case 16: UNET_FUSED(MODE, D, 16); break;  \
-        case 8: UNET_FUSED(MODE, D, 8); break;    \
-        case 4: UNET_FUSED(MODE, D, 4); break;    \
-        case 2: UNET_FUSED(MODE, D, 2); break;    \
-        default: UNET_FUSED(MODE, D, 1); break;   \
-    }
-#define UNET_FUSED_D(MODE)                        \
-    if (drop) {                                   \
-        UNET_FUSED_QT(MODE, true)                 \
-    } else {                                      \
-        UNET_FUSED_QT(MODE, false)                \
-    }
-    switch (mode) {
-        case UNET_VIEW_PLAIN: UNET_FUSED_D(UNET_VIEW_PLAIN) break;
-        case UNET_VIEW_BNRELU: UNET_FUSED_D(UNET_VIEW_BNRELU) break;
-        case UNET_VIEW_POOL_BNRELU: UNET_FUSED_D(UNET_VIEW_POOL_BNRELU) break;
-        default: UNET_FUSED_D(UNET_VIEW_CONCAT) break;
-    }
-#undef UNET_FUSED_D
-#undef UNET_FUSED_QT
-#undef UNET_FUSED
-    UNET_CHECK_LAUNCH("dwconv3x3_bwd_fused(tiled)");
-    return 0;
-}
 
 size_t dw_tiled_filter_partials(int N, int H, int W, int C) {
     TilePlan p = tile_plan(N, H, W, C);

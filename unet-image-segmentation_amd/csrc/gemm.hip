@@ -29,7 +29,6 @@ size_t colsum_workspace(int64_t rows, int cols);
 namespace {
 
 constexpr int BK = 16;
-constexpr int kStatsRows = 128;  // rows per BatchNorm partial (= BM of the stats GEMM)
 
 // A_BNBWD: A = dz of a BatchNorm + ReLU (+ dropout) output, formed on load from the incoming
 // gradient da (a.src0) and the raw pre-BN z: g = da * drop * [z*sc+sh > 0],
@@ -1077,27 +1076,19 @@ bool rows_vec_ok(const RowsArgs& a, int amode) {
 // Chosen per operand mode from lab timings (tools/lab/gemm_lab.hip) on the U-Net shapes:
 // the BatchNorm-backward data gradient forms its A operand per N-tile, so it prefers the
 // 256-wide tile when the grid still fills the chip, and BK = 32 otherwise; plain operands
-// take BK = 32 from K = 256 on.  UNET_ROWS_CFG="BN,BK" overrides (tuning only).
+// take BK = 32 from K = 256 on.  Lab build: UNET_ROWS_BN / UNET_ROWS_BK override (tuning only).
 struct RowsCfg {
     int bn, bk;
 };
 RowsCfg rows_cfg(const RowsArgs& a, int amode) {
-    static int env_bn = -1, env_bk = 0;
-    if (env_bn < 0) {
-        env_bn = 0;
-        if (const char* e = getenv("UNET_ROWS_CFG")) sscanf(e, "%d,%d", &env_bn, &env_bk);
-    }
-    if (env_bn > 0) return RowsCfg{env_bn, env_bk};
+    const int env_bn = lab_knob("UNET_ROWS_BN", 0);
+    if (env_bn > 0) return RowsCfg{env_bn, lab_knob("UNET_ROWS_BK", 16)};
     if (amode == A_BNBWD) {
         if (a.N <= 64) return RowsCfg{64, 32};
         if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
         return RowsCfg{128, 32};
     }
-    static int bk32_k = -1;  // smallest K that takes BK = 32 (UNET_BK32_MIN_K: tuning)
-    if (bk32_k < 0) {
-        const char* e = getenv("UNET_BK32_MIN_K");
-        bk32_k = e ? atoi(e) : 256;
-    }
+    const int bk32_k = lab_knob("UNET_BK32_MIN_K", 256);  // smallest K that takes BK = 32
     if (a.N <= 64) return RowsCfg{64, 16};
     return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
@@ -1146,12 +1137,8 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     w.bp = P > 64 ? 128 : 64;
     w.bq = Q > 64 ? 128 : 64;
     w.tiles = (int)(cdiv(P, w.bp) * cdiv(Q, w.bq));
-    static int target = -1;  // ~4 blocks per CU (UNET_WGRAD_BLOCKS: tuning; read once per process)
-    if (target < 0) {
-        const char* e = getenv("UNET_WGRAD_BLOCKS");
-        target = e ? atoi(e) : 1024;
-        if (target < 1) target = 1024;
-    }
+    int target = lab_knob("UNET_WGRAD_BLOCKS", 1024);  // ~4 blocks per CU
+    if (target < 1) target = 1024;
     int64_t want = cdiv(target, w.tiles);
     int64_t maxs = M / 512;               // >= 32 k-steps per block: fewer, cheaper slabs
     if (maxs < 1) maxs = 1;
@@ -1211,8 +1198,6 @@ int run_wgrad(WgradArgs a, int amode, int bmode, float* out, void* ws, size_t ws
             launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, true>(a, w, st);
         else
             launch_wgrad_t<W_UNSHUFFLE, false, W_PLAIN, false>(a, w, st);
-    } else if (amode == W_PLAIN && bmode == W_BNBWD) {
-        launch_wgrad_t<W_PLAIN, false, W_BNBWD, false>(a, w, st);
     } else if (amode == W_BNRELU && bmode == W_PLAIN) {
         if (ad)
             launch_wgrad_t<W_BNRELU, true, W_PLAIN, false>(a, w, st);
@@ -1446,27 +1431,6 @@ extern "C" int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_
     return run_wgrad(a, W_PLAIN, W_PLAIN, d_pw_kernel, ws, ws_bytes, as_stream(stream), "unet_pointwise_bwd_filter");
 }
 
-extern "C" int unet_pointwise_bwd_filter_bnrelu(const float* y, const float* da, const float* z, int64_t m, int cin,
-                                                int cout, const float* scale, const float* shift, const float* coef,
-                                                float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
-    const char* op = "unet_pointwise_bwd_filter_bnrelu";
-    UNET_CHECK_ARG(y && da && z && scale && shift && coef && d_pw_kernel, "%s: null pointer", op);
-    UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0 && cin % 4 == 0 && cout % 4 == 0, "%s: bad sizes", op);
-    UNET_CHECK_ARG(((uintptr_t)y | (uintptr_t)da | (uintptr_t)z | (uintptr_t)scale | (uintptr_t)shift |
-                    (uintptr_t)coef) % 16 == 0, "%s: operands must be 16-B aligned", op);
-    WgradArgs a{};
-    a.a = plain_view(y, cin);
-    a.P = cin;
-    a.b = plain_view(da, cout);
-    a.b.sc0 = scale;
-    a.b.sh0 = shift;
-    a.bz = z;
-    a.bcoef = coef;
-    a.Q = cout;
-    a.M = m;
-    return run_wgrad(a, W_PLAIN, W_BNBWD, d_pw_kernel, ws, ws_bytes, as_stream(stream), op);
-}
-
 // ------------------------------------------------------------ transposed conv 2x2/2 ----
 extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
                                           const float* bias, float* out, unet_stream_t stream) {
@@ -1501,13 +1465,8 @@ extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int 
 }
 
 namespace {
-bool convt_fused_bias() {  // UNET_CONVT_FUSED_BIAS=0: separate colsum pass (A/B switch)
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("UNET_CONVT_FUSED_BIAS");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    return on == 1;
+bool convt_fused_bias() {  // lab build UNET_CONVT_FUSED_BIAS=0: separate colsum pass (A/B switch)
+    return lab_knob("UNET_CONVT_FUSED_BIAS", 1) != 0;
 }
 }  // namespace
 

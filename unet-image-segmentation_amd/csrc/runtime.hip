@@ -222,6 +222,16 @@ int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t
 
 }  // namespace unet
 
+#ifdef UNET_LAB_BUILD
+#include <cstdlib>
+namespace unet {
+int lab_knob(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+}  // namespace unet
+#endif
+
 namespace unet {
 namespace {
 __global__ __launch_bounds__(256) void copy_strided_kernel(const float* __restrict__ src, int64_t rows, int cols,

@@ -157,10 +157,11 @@ class UNetEngine:
         self.recompute_y = os.environ.get("UNET_RECOMPUTE_Y", "1") != "0"
         # issue a y-recomputing block's fused weight gradient (one 111 KB-LDS block per CU for the
         # launch's whole length) only after the main stream has issued the NEXT block's statistics
-        # finish, instead of beside its own depthwise data gradient (single-process runs only: with
-        # a gradient hook the all-reduce low-water mark must not overtake it)
+        # finish, instead of beside its own depthwise data gradient (under data parallelism the
+        # all-reduce low-water report waits for the deferred launch, see _grads_ready)
         self.defer_sw = os.environ.get("UNET_SW_DEFER", "1") != "0"
         self._pending_side = None
+        self._pending_ready: Optional[str] = None
         self._ev = None  # created on first use (on the device)
 
     # ------------------------------------------------------------------ weights ------
@@ -412,18 +413,26 @@ class UNetEngine:
             fn()
 
     def _flush_side(self):
-        """Issue the deferred side-stream weight gradients (UNET_SW_DEFER), if any."""
+        """Issue the deferred side-stream weight gradients (UNET_SW_DEFER), if any, then report
+        the gradient low-water mark that waited for them."""
         if self._pending_side is not None:
             fn, self._pending_side = self._pending_side, None
             self._side_wait_main()
             with torch.cuda.stream(self.side):
                 fn()
+            name, self._pending_ready = self._pending_ready, None
+            if name is not None:
+                self._grads_ready(name)
 
     def _grads_ready(self, name: str):
         """Gradients at flat offsets >= offset(name) are final once both streams get here:
         the hook (bucketed all-reduce) is issued from the side stream after it has caught up
-        with the main stream."""
+        with the main stream.  While a block's weight gradients are deferred the report waits
+        for them (_flush_side), so no bucket is reduced before its last writer is issued."""
         if self.grad_hook is not None:
+            if self._pending_side is not None:
+                self._pending_ready = name  # the lowest offset reported so far wins
+                return
             if self.overlap:
                 self._side_wait_main()
                 with torch.cuda.stream(self.side):
@@ -503,7 +512,7 @@ class UNetEngine:
         # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
         if self.overlap and dx0 is not None:
             self._flush_side()
-            if self.defer_sw and bb.y_recompute and self.grad_hook is None:
+            if self.defer_sw and bb.y_recompute:
                 self._pending_side = weight_grads
             else:
                 self._side_wait_main()

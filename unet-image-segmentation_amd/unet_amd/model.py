@@ -160,7 +160,7 @@ class UNetModel:
         cbs = CallbackList(callbacks or [], self)
         hist = History()
         self.stop_training = False
-        it = iter(self._prefetch(x))
+        it = iter(self._prefetch(x, epochs * (steps_per_epoch or 1)))
         cbs.on_train_begin()
         for epoch in range(epochs):
             cbs.on_epoch_begin(epoch)
@@ -196,12 +196,14 @@ class UNetModel:
             it.close()
         return hist
 
-    def _prefetch(self, data):
-        """Wrap a host-batch iterable in the background decoder / async H2D prefetcher."""
+    def _prefetch(self, data, limit: int):
+        """Wrap a host-batch iterable in the background decoder / async H2D prefetcher.  It reads
+        at most `limit` batches (the steps the caller takes), so a single-pass generator shared
+        across fit / evaluate calls (a Keras-style flow) loses nothing to read-ahead."""
         from .prefetch import Prefetcher
         if isinstance(data, Prefetcher) or not hasattr(data, "__iter__"):
             return data
-        return Prefetcher(data, self.engine.device)
+        return Prefetcher(data, self.engine.device, limit=limit)
 
     def sync_bn_statistics(self):
         """Data parallel: average the BatchNorm moving statistics over the ranks (tf.distribute
@@ -213,7 +215,7 @@ class UNetModel:
             average_(self.engine.stats, self.bucketer.group)
 
     def evaluate(self, data, steps: Optional[int] = None, prefix: str = "") -> Dict[str, float]:
-        it = iter(self._prefetch(data))
+        it = iter(self._prefetch(data, steps or 1))
         if self.mean_iou is not None:
             saved = self.mean_iou.confusion.clone()
             self.mean_iou.reset_state()

@@ -267,29 +267,6 @@ def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Te
           _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
 
 
-def dwconv3x3_bwd_slabs(x: View, n, h, w) -> int:
-    """Slab count of dwconv3x3_bwd's BN partials (0: no fused data + filter path for this shape)."""
-    vs = x.c_struct()
-    return L.query("unet_dwconv3x3_bwd_slabs", ctypes.byref(vs), n, h, w)
-
-
-def dwconv3x3_bwd(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Optional[Tensor], dx1: Optional[Tensor],
-                  ddk: Tensor, mean=None, rstd=None, partials: Optional[Tensor] = None):
-    """Depthwise data + filter gradient in one pass over dy (+ the view block's BN partials)."""
-    C = x.channels
-    _check(dk, "depthwise_kernel", 9 * C)
-    _check(dy, "dy", n * h * w * C)
-    _check(ddk, "d_depthwise_kernel", 9 * C)
-    if partials is not None:
-        _check(partials, "bn_partials", bn_stats_partials_numel(dwconv3x3_bwd_slabs(x, n, h, w), C))
-    ws, wsb = _ws(L.query("unet_dwconv3x3_bwd_workspace", n, h, w, C), dy.device)
-    vs = x.c_struct()
-    m = n * h * w
-    nb = 2 * x.src_bytes(n, h, w) + 8.0 * m * C
-    _call("unet_dwconv3x3_bwd", (36.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy), _ptr(dx0),
-          _ptr(dx1), _ptr(ddk), _ptr(mean), _ptr(rstd), _ptr(partials), ws, wsb, _stream())
-
-
 def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
     C = x.channels
     _check(dy, "dy", n * h * w * C)
@@ -330,20 +307,6 @@ def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
     ws, wsb = _ws(L.query("unet_pointwise_bwd_filter_workspace", m, cin, cout), y.device)
     _call("unet_pointwise_bwd_filter", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(y),
           _ptr(dz), m, cin, cout, _ptr(dpk), ws, wsb, _stream())
-
-
-def pointwise_bwd_filter_bnrelu(y: Tensor, da: Tensor, z: Tensor, m: int, cin: int, cout: int, scale: Tensor,
-                                shift: Tensor, coef: Tensor, dpk: Tensor):
-    """pointwise_bwd_filter with dz formed on load from (da, z) and the BN-backward coefficients."""
-    _check(y, "y", m * cin)
-    _check(da, "da", m * cout)
-    _check(z, "z", m * cout)
-    _check(coef, "coef", 3 * cout)
-    _check(dpk, "d_pointwise_kernel", cin * cout)
-    ws, wsb = _ws(L.query("unet_pointwise_bwd_filter_workspace", m, cin, cout), y.device)
-    _call("unet_pointwise_bwd_filter_bnrelu", (2.0 * m * cin * cout, 4.0 * (m * cin + 2 * m * cout + cin * cout)),
-          _ptr(y), _ptr(da), _ptr(z), m, cin, cout, _ptr(scale), _ptr(shift), _ptr(coef), _ptr(dpk), ws, wsb,
-          _stream())
 
 
 SEPCONV_AUTO, SEPCONV_TILE, SEPCONV_RK = 0, 1, 2

@@ -28,10 +28,14 @@ class Prefetcher:
     """Iterates `source` (yielding (x, y) numpy batches, optionally with .global_size) and yields
     (x, y) device tensors (a `data.Shard` when the source batch carries global_size)."""
 
-    def __init__(self, source: Iterable, device=None, depth: int = 3):
+    def __init__(self, source: Iterable, device=None, depth: int = 3, limit: Optional[int] = None):
+        """limit: pull at most this many batches from `source` per iteration, so a single-pass
+        generator shared with the caller loses no batches to read-ahead (model.fit / evaluate
+        pass the number of steps they will take)."""
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.source = source
+        self.limit = limit
         self.device = torch.device(device) if device is not None else None
         self.depth = depth
         self._q: Optional[queue.Queue] = None
@@ -48,15 +52,19 @@ class Prefetcher:
             d = pinned.to(self.device, non_blocking=True)
         return d, pinned
 
-    def _run(self):
+    def _run(self, q: "queue.Queue", stop: threading.Event):
+        """Producer of ONE iteration: it only ever touches its own queue and stop event, so a
+        thread that outlives its iteration cannot feed a later one."""
         stream = None
         try:
             if self.device is not None and self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
                 stream = torch.cuda.Stream(device=self.device)
+            taken = 0
             for batch in self.source:
-                if self._stop.is_set():
+                if stop.is_set():
                     break
+                taken += 1
                 x, y = batch[0], batch[1]
                 gsz = getattr(batch, "global_size", None)
                 xd, xp = self._to_device(x, stream)
@@ -66,30 +74,31 @@ class Prefetcher:
                     ev = torch.cuda.Event()
                     ev.record(stream)
                 item = (xd, yd, gsz, ev, (xp, yp))  # pinned buffers stay referenced until consumed
-                while not self._stop.is_set():
-                    try:
-                        self._q.put(item, timeout=0.1)
-                        break
-                    except queue.Full:
-                        continue
-            self._put_final(_END)
+                if not self._put(q, stop, item):
+                    break
+                if self.limit is not None and taken >= self.limit:
+                    break
+            self._put(q, stop, _END)
         except BaseException as e:  # surfaced in the consumer
-            self._put_final(_Failure(e))
+            self._put(q, stop, _Failure(e))
 
-    def _put_final(self, item):
-        while not self._stop.is_set():
+    @staticmethod
+    def _put(q, stop, item) -> bool:
+        while not stop.is_set():
             try:
-                self._q.put(item, timeout=0.1)
-                return
+                q.put(item, timeout=0.1)
+                return True
             except queue.Full:
                 continue
+        return False
 
     # ------------------------------------------------------------------ consumer ---
     def __iter__(self):
         self.close()
-        self._stop.clear()
+        self._stop = threading.Event()  # per iteration: see _run
         self._q = queue.Queue(maxsize=self.depth)
-        self._thread = threading.Thread(target=self._run, name="unet-prefetch", daemon=True)
+        self._thread = threading.Thread(target=self._run, args=(self._q, self._stop), name="unet-prefetch",
+                                        daemon=True)
         self._thread.start()
         return self
 
@@ -114,11 +123,17 @@ class Prefetcher:
             return Shard(xd, yd, gsz)
         return xd, yd
 
-    def close(self):
+    def close(self, timeout: float = 60.0):
+        """Stop the producer and wait for it.  It notices the stop flag between batches, so this
+        waits at most for the batch the source is producing; a producer still alive after
+        `timeout` (a source blocked inside next()) raises rather than letting a new iteration call
+        into the same source concurrently."""
         self._stop.set()
         t = self._thread
-        if t is not None and t.is_alive():
-            t.join(timeout=5.0)
+        if t is not None and t.is_alive() and t is not threading.current_thread():
+            t.join(timeout=timeout)
+            if t.is_alive():
+                raise RuntimeError("Prefetcher: the producer thread did not stop (source blocked in next())")
         self._thread = None
         self._q = None
 
