@@ -1,6 +1,7 @@
 """Variable inventory of U_NET (model/u_net.py) and host logic: names, Keras layouts, counts,
 initializers, the flat HBM layout, the builder's ValueError, callbacks."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -114,3 +115,37 @@ def test_callbacks_semantics():
         m.w = [np.full(1, float(e))]
         es.on_epoch_end(e, {"val_mean_io_u": v})
     assert m.stop_training and m.w[0][0] == 1.0 and es.stopped_epoch == 3
+    # the report scripts/train.py prints after fit (reference scripts/train.py:317-331)
+    from scripts.train import training_summary
+
+    class H:
+        history = {"val_mean_io_u": [0.5, 0.7, 0.6, 0.6]}
+    assert training_summary(H(), es, "val_mean_io_u", "max", 30) == [
+        "Early stopping triggered at epoch 4",
+        "Best monitored score (val_mean_io_u): 0.7000 (from epoch 2)"]  # 4 - patience 2
+    es2 = EarlyStopping("val_mean_io_u", patience=10, mode="max")
+    es2.on_train_begin()
+    assert training_summary(H(), es2, "val_mean_io_u", "max", 4) == [
+        "Best monitored score (val_mean_io_u): 0.7000 (from epoch 2)"]
+    assert training_summary(H(), es2, "val_loss", "min", 4) == [
+        "Best monitored score (val_loss): inf (from epoch N/A)"]
+
+
+def test_train_sample_count_fallback(tmp_path, capsys):
+    """scripts/train.py counts samples from the loaders, else lists the frame directories, else
+    exits 1 (reference scripts/train.py:237-249)."""
+    from scripts.train import TRAIN_FRAMES_DIR, VAL_FRAMES_DIR, count_samples
+
+    class Bad:
+        @property
+        def samples(self):
+            raise RuntimeError("no count")
+    for d, n in ((TRAIN_FRAMES_DIR, 3), (VAL_FRAMES_DIR, 2)):
+        os.makedirs(tmp_path / d)
+        for i in range(n):
+            (tmp_path / d / f"{i}.png").write_bytes(b"")
+    assert count_samples(Bad(), Bad(), str(tmp_path)) == (3, 2)
+    assert "(Fallback) Counted 3 train files, 2 val files." in capsys.readouterr().out
+    with pytest.raises(SystemExit) as e:
+        count_samples(Bad(), Bad(), str(tmp_path / "missing"))
+    assert e.value.code == 1

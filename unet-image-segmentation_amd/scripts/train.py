@@ -61,6 +61,51 @@ def parse_args(argv=None) -> argparse.Namespace:
     return parser.parse_args(argv)
 
 
+def count_samples(train, val, root="."):
+    """Sample counts from the loaders, falling back to listing the frame directories when a loader
+    cannot report them (reference scripts/train.py:237-249).  Exits 1 if neither works."""
+    try:
+        n_train, n_val = train.samples, val.samples
+        print(f"Found {n_train} training samples and {n_val} validation samples.")
+    except Exception as e:
+        print(f"Warning: Could not read sample count from generators ({e}). Falling back to file listing.")
+        try:
+            n_train = len(os.listdir(os.path.join(root, TRAIN_FRAMES_DIR)))
+            n_val = len(os.listdir(os.path.join(root, VAL_FRAMES_DIR)))
+            print(f"(Fallback) Counted {n_train} train files, {n_val} val files.")
+        except FileNotFoundError as fe:
+            print(f"Error counting files: {fe}. Please check dataset paths.")
+            sys.exit(1)
+    return n_train, n_val
+
+
+def training_summary(history, early_stopping, monitor_metric, monitor_mode, epochs):
+    """The report after model.fit (reference scripts/train.py:317-331): the early-stopping epoch
+    if it triggered, the best monitored score, and the epoch it came from with the reference's
+    own arithmetic (stopped epoch - patience when early stopping fired, else argmax + 1 for a
+    'max' monitor, else 'N/A')."""
+    lines = []
+    best = np.inf if monitor_mode == "min" else -np.inf
+    stopped = epochs
+    fired = early_stopping is not None and early_stopping.stopped_epoch > 0
+    if fired:
+        stopped = early_stopping.stopped_epoch + 1
+        lines.append(f"Early stopping triggered at epoch {stopped}")
+        best = early_stopping.best
+    else:
+        scores = history.history.get(monitor_metric)
+        if scores:
+            best = min(scores) if monitor_mode == "min" else max(scores)
+    if fired:
+        at = stopped - early_stopping.patience
+    elif monitor_mode == "max" and monitor_metric in history.history:
+        at = int(np.argmax(history.history[monitor_metric])) + 1
+    else:
+        at = "N/A"
+    lines.append(f"Best monitored score ({monitor_metric}): {best:.4f} (from epoch {at})")
+    return lines
+
+
 def main(argv=None):
     args = parse_args(argv)
     from unet_amd.callbacks import EarlyStopping, JSONLogger, ModelCheckpoint, ReduceLROnPlateau
@@ -124,22 +169,30 @@ def main(argv=None):
     if rank == 0:
         model.summary(line_length=100)
 
-    n_train, n_val = train.samples, val.samples
-    say(f"Found {n_train} training samples and {n_val} validation samples.")
+    if rank == 0:
+        n_train, n_val = count_samples(train, val, args.dataset_root)
+    else:
+        n_train, n_val = train.samples, val.samples
     if n_train == 0 or n_val == 0:
         print("Error: No training or validation images found/loaded. Check dataset paths and contents.")
         sys.exit(1)
     steps_per_epoch = max(1, n_train // args.batch_size)
     validation_steps = max(1, n_val // args.batch_size)
     say(f"Steps per epoch: {steps_per_epoch}, Validation steps: {validation_steps}")
+    if n_train < args.batch_size:
+        say(f"Warning: Training dataset size ({n_train}) < batch size ({args.batch_size}).")
+    if n_val < args.batch_size:
+        say(f"Warning: Validation dataset size ({n_val}) < batch size ({args.batch_size}).")
 
     monitor_metric, monitor_mode = "val_mean_io_u", "max"
     say(f"Setting up Callbacks - Monitoring: '{monitor_metric}' (mode: {monitor_mode})")
     model_dir = os.path.dirname(args.model_out)
     if model_dir:
         os.makedirs(model_dir, exist_ok=True)
-    callbacks = [EarlyStopping(monitor=monitor_metric, patience=10, mode=monitor_mode, restore_best_weights=True,
-                               verbose=1 if rank == 0 else 0),
+        say(f"Ensured model save directory exists: {model_dir}")
+    early_stopping = EarlyStopping(monitor=monitor_metric, patience=10, mode=monitor_mode, restore_best_weights=True,
+                                   verbose=1 if rank == 0 else 0)
+    callbacks = [early_stopping,
                  ReduceLROnPlateau(monitor=monitor_metric, factor=0.2, patience=3, mode=monitor_mode, min_lr=1e-6,
                                    verbose=1 if rank == 0 else 0)]
     if rank == 0:
@@ -154,9 +207,8 @@ def main(argv=None):
         history = model.fit(train, epochs=args.epochs, steps_per_epoch=steps_per_epoch, validation_data=val,
                             validation_steps=validation_steps, callbacks=callbacks, verbose=1 if rank == 0 else 0)
         say("\n--- Training complete ---")
-        scores = history.history.get(monitor_metric, [])
-        if scores:
-            say(f"Best monitored score ({monitor_metric}): {max(scores):.4f} (from epoch {int(np.argmax(scores)) + 1})")
+        for line in training_summary(history, early_stopping, monitor_metric, monitor_mode, args.epochs):
+            say(line)
         say(f"Best model saved to: {args.model_out}")
     except KeyboardInterrupt:
         print("\n--- Training interrupted by user ---")
