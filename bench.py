@@ -40,8 +40,16 @@ ROOFLINE_OP = "unet_pointwise_fwd"
 RIDGE = PEAK_FP32_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # flop/B
 
 
+# the kernel set a PMC kernel regex (tools/pmc_traffic.py) counts, per op: the route label of
+# the KernelTimer records that launch exactly those kernels
+PMC_ROUTE = {"unet_pointwise_bwd_data_bnrelu": "gemm_bnbwd"}
+
+
 def roofline_obj(op, s, steps):
-    """Roofline object for one C-ABI op from KernelTimer totals (algorithmic flops / bytes)."""
+    """Roofline object for one C-ABI op from KernelTimer totals (algorithmic flops / bytes).
+    `frac` uses the op's dominant bound over all its launches; `frac_per_launch_bound` prices
+    every launch against its own bound (sum of max(flops/peak, bytes/peak) over launches / time),
+    so HBM-bound launches of an MFMA-labelled op are not charged at the MFMA peak."""
     sec = s["ms"] * 1e-3
     mfma = s["bytes"] == 0 or s["flops"] / s["bytes"] >= RIDGE
     if mfma:
@@ -49,11 +57,24 @@ def roofline_obj(op, s, steps):
     else:
         ach, peak, unit = s["bytes"] / sec / 1e9, PEAK_HBM_GBS, "GB/s"
     traffic, tsrc = pmc_traffic(op)
-    return {"bound": "mfma" if mfma else "hbm", "kernel": op, "achieved": round(ach, 2), "peak": peak,
-            "unit": unit, "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": tsrc,
-            "algorithmic_bytes_per_launch": round(s["bytes"] / s["launches"]),
-            "algorithmic_flops_per_launch": round(s["flops"] / s["launches"]),
-            "launches_per_step": s["launches"] // steps, "avg_launch_us": round(s["ms"] / s["launches"] * 1e3, 2)}
+    out = {"bound": "mfma" if mfma else "hbm", "kernel": op, "achieved": round(ach, 2), "peak": peak,
+           "unit": unit, "frac": round(ach / peak, 4),
+           "frac_per_launch_bound": round(s["t_roof_ms"] / s["ms"], 4),
+           "hbm_bound_launches_per_step": s["hbm_bound_launches"] // steps,
+           "traffic": traffic, "traffic_source": tsrc,
+           "algorithmic_bytes_per_launch": round(s["bytes"] / s["launches"]),
+           "algorithmic_flops_per_launch": round(s["flops"] / s["launches"]),
+           "launches_per_step": s["launches"] // steps, "avg_launch_us": round(s["ms"] / s["launches"] * 1e3, 2)}
+    r = s["routes"].get(PMC_ROUTE.get(op, "main"))
+    if r:
+        # the launch set the PMC regex counts: its algorithmic bytes and measured time per launch
+        ab = r["bytes"] / r["launches"]
+        out["pmc_launch_set"] = {"route": PMC_ROUTE.get(op, "main"), "launches_per_step": r["launches"] // steps,
+                                 "algorithmic_bytes_per_launch": round(ab),
+                                 "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 2),
+                                 "traffic_over_algorithmic": round(traffic / ab, 3) if traffic else None,
+                                 "frac_per_launch_bound": round(r["t_roof_ms"] / r["ms"], 4)}
+    return out
 
 
 def op_breakdown(summary):
@@ -74,11 +95,11 @@ def encoder_block_roofline(batch, size, device, reps=10):
     step) at `batch` images, each timed with HIP events around `reps` back-to-back launches (median
     of 3 groups), against
     t_roof = max(flops / peak_fp32, bytes / peak_hbm) with flops = px(18 Cin + 2 Cin Cout) and
-    bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Uses the engine's kernel choice
-    (fused unet_sepconv_fwd where supported, dw + pw launches for the 3-channel first block), and
-    stores the depthwise output y only where the train step does."""
+    bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Runs the train step's own kernel
+    choice per block (engine.block_fwd_choice: the same launches, y stores included)."""
     import torch
     from unet_amd import ops
+    from unet_amd.engine import block_fwd_choice
     from unet_amd.ops import View
     g = torch.Generator(device="cpu").manual_seed(7)
     filters = (64, 128, 256, 512)
@@ -99,13 +120,13 @@ def encoder_block_roofline(batch, size, device, reps=10):
             dk = torch.randn((3, 3, ck, 1), generator=g).to(device)
             pk = (torch.randn((1, 1, ck, co), generator=g) / ci ** 0.5).to(device)
             m = batch * hh * hh
-            # y (the depthwise output) is stored only where the train step keeps it: blocks whose
-            # weight gradients recompute it from the view (unet_sepconv_bwd_filter) do not
-            keep_y = not ops.sepconv_bwd_filter_supported(view, batch, hh, hh, co)
+            # the train step's own kernel choice (engine.block_fwd_choice): fused launch from the
+            # 64 x 64 level up, y stored unless the block's weight gradients recompute it; split
+            # depthwise + pointwise launches (y always stored) below
+            fused, keep_y = block_fwd_choice(view, batch, hh, hh, co, training=True)
             ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
             part = torch.zeros(ops.bn_partials_numel(m, co), device=device)
-            fused = ops.sepconv_supported(view, batch, hh, hh, co)
 
             def run():
                 if fused:
@@ -129,7 +150,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
             nb = 4.0 * (m * (ci + co) + 9 * ci + ci * co + 4 * co)
             t_roof = max(fl / (PEAK_FP32_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)) * 1e6
             rows.append({"block": f"enc{lvl + 1}_block{blk + 1}", "hw": hh, "cin": ci, "cout": co,
-                         "kernel": ("unet_sepconv_fwd" if fused else "dwconv3x3_fwd+pointwise_fwd") +
+                         "kernel": ("unet_sepconv_fwd" + (" (+y store)" if keep_y else "") if fused
+                                    else "dwconv3x3_fwd+pointwise_fwd") +
                                    (f" (input padded {ci}->{ck} ch)" if ck != ci else ""),
                          "bound": "mfma" if fl / nb >= RIDGE else "hbm", "us": round(us, 1),
                          "t_roof_us": round(t_roof, 1), "frac": round(t_roof / us, 4),

@@ -190,12 +190,86 @@ def train128_fixture():
     return out
 
 
+SUB = 16384  # gradient elements kept per tensor in the training-geometry fixtures
+
+
+def sub_index(size):
+    """Deterministic strided subsample of a flat tensor (all of it when it is small)."""
+    if size <= SUB:
+        return np.arange(size)
+    return (np.arange(SUB, dtype=np.int64) * size) // SUB
+
+
+def class_masks(n, h, w, ncls, seed):
+    """One-hot class maps for the multi-class geometry: 8x8-pixel cells of uniformly drawn classes."""
+    cells = np.floor(U(seed, (n, h // 8, w // 8)) * ncls).astype(np.int64).clip(0, ncls - 1)
+    cls = cells.repeat(8, 1).repeat(8, 2)
+    return np.eye(ncls)[cls]
+
+
+def train_big_fixture(size, n, ncls, x_seed, w_seed):
+    """One train step (dropout 0) at a BASELINE training geometry, full widths, float64 oracle:
+    loss, dice, every block's BatchNorm batch mean / variance, every gradient's norm, first 128
+    values and a strided subsample (sub_index) with e32 = the same step in float32 (its own
+    relative-L2 distance to float64 on that subsample, and over the whole tensor), and the first
+    256 post-AdamW values of every variable (moving statistics included).  Too slow to run live on
+    the GPU box (about 4 minutes at 256x256 x 16 here), so the box only compares."""
+    w = model_weights(ncls, FULL, w_seed)
+    x = U(x_seed, (n, size, size, 3))
+    y = quad_masks(n, size, size) if ncls == 1 else class_masks(n, size, size, ncls, x_seed + 1)
+    orc = UNetOracle(ncls, 0.0)
+    out = {"x_seed": x_seed, "w_seed": w_seed, "n": n, "size": size, "ncls": ncls}
+    prob, cache, stats = orc.forward(w, x, training=True)
+    lval, dprob = orc.loss_and_dprob(y, prob)
+    out["loss"], out["dice"] = lval, K.dice_coef(y, prob)
+    for name, rec in cache.items():
+        if isinstance(rec, dict) and "mean" in rec:
+            out["bn_mean:" + name], out["bn_var:" + name] = rec["mean"], rec["var"]
+    del prob
+    g, _ = orc.backward(w, cache, dprob)
+    del cache, dprob
+    for k, v in g.items():
+        flat = v.reshape(-1)
+        out["gnorm:" + k] = np.linalg.norm(flat)
+        out["g128:" + k] = flat[:128]
+        out["gsub:" + k] = flat[sub_index(flat.size)].astype(np.float32)
+    for k, v in w.items():
+        if k in g:
+            p1, _, _ = K.adamw_update(v, g[k], np.zeros_like(v), np.zeros_like(v), 1, 2e-3, 1e-4)
+        else:
+            p1 = stats[k]
+        out["new256:" + k] = p1.reshape(-1)[:256]
+    w32 = {k: v.astype(np.float32) for k, v in w.items()}
+    prob32, cache32, _ = orc.forward(w32, x.astype(np.float32), training=True)
+    _, dprob32 = orc.loss_and_dprob(y.astype(np.float32), prob32)
+    del prob32
+    g32, _ = orc.backward(w32, cache32, dprob32)
+    del cache32
+    for k, v in g.items():
+        a, b = g32[k].reshape(-1).astype(np.float64), v.reshape(-1)
+        out["e32:" + k] = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        i = sub_index(b.size)
+        out["e32sub:" + k] = np.linalg.norm(a[i] - b[i]) / max(np.linalg.norm(b[i]), 1e-30)
+    return out
+
+
+def train256_fixture():
+    """configs[1]: 256x256x3 binary, batch 16 (the geometry scripts/train.py trains at, :84-88)."""
+    return train_big_fixture(256, 16, 1, 51, 11)
+
+
+def train256c21_fixture():
+    """configs[4] per GPU: 256x256x3, 21 classes (softmax head), batch 8."""
+    return train_big_fixture(256, 8, 21, 61, 12)
+
+
 def write(name, d):
     np.savez_compressed(os.path.join(HERE, name), **{k.replace("/", "|"): v for k, v in d.items()})
 
 
 BIG = {"fwd256.npz": fwd256_fixture, "fwd512.npz": fwd512_fixture, "fwd21.npz": fwd21_fixture,
-       "samples.npz": samples_fixture, "train128.npz": train128_fixture}
+       "samples.npz": samples_fixture, "train128.npz": train128_fixture, "train256.npz": train256_fixture,
+       "train256c21.npz": train256c21_fixture}
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:  # regenerate only the named fixtures

@@ -195,3 +195,89 @@ def test_train_step_128_batch4():
             gd = grads[name].reshape(-1)[:256]
             own, _, _ = K.adamw_update(w0, gd, np.zeros_like(w0), np.zeros_like(w0), 1, 2e-3, 1e-4)
             assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name
+
+
+@pytest.mark.parametrize("fixture", ["train256.npz", "train256c21.npz"])
+def test_train_step_training_geometry(fixture):
+    """One train step at the geometry the reference trains at (scripts/train.py:84-88, 256x256)
+    with configs[1]'s batch of 16 (binary) and configs[4]'s per-GPU batch of 8 (21 classes),
+    against the committed float64 oracle step (tests/golden/make_golden.py train_big_fixture; the
+    oracle takes ~4 minutes at this size, so the box only compares):
+      * loss and dice within 1e-5;
+      * every block's BatchNorm batch mean / variance (1,048,576 pixels per channel at 256 x 16)
+        within 1e-4 relative to the channel's scale;
+      * every gradient tensor on its strided subsample within relative L2 max(2e-3, 2 e32), e32 =
+        the float32 oracle's own distance to float64 there; norms within 1e-2;
+      * post-AdamW values as test_train_step_128_batch4 (first 128 per variable) and the moving
+        statistics."""
+    from unet_amd.engine import BN_EPS
+    from unet_amd.model import UNetModel
+    from unet_amd.optim import AdamW
+    g = _load(fixture)
+    size, n, ncls = int(g["size"]), int(g["n"]), int(g["ncls"])
+    m = UNetModel((size, size, 3), ncls, dropout_rate=0.0)
+    w = MG.model_weights(ncls, MG.FULL, int(g["w_seed"]))
+    m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+    x = MG.U(int(g["x_seed"]), (n, size, size, 3))
+    y = MG.quad_masks(n, size, size) if ncls == 1 else MG.class_masks(n, size, size, ncls, int(g["x_seed"]) + 1)
+    m.compile(AdamW(2e-3, 1e-4), "dice_loss")
+    res = m.train_step(x.astype(np.float32), y.astype(np.float32)).cpu().numpy()
+    torch.cuda.synchronize()
+    grads = {k: host(t) for k, t in m.engine.gvars.items()}
+    neww = m.engine.get_weights_dict()
+    # BatchNorm batch statistics of every block
+    A = m.engine._acts_last
+    bn_worst = 0.0
+    for b in m.engine.blocks:
+        bb = A.blocks[b.name]
+        mu, var = g["bn_mean:" + b.name], g["bn_var:" + b.name]
+        dmu = host(bb.mean).astype(np.float64)
+        dvar = 1.0 / host(bb.rstd).astype(np.float64) ** 2 - BN_EPS
+        sd = np.sqrt(var + BN_EPS)
+        e = max(float(np.abs(dmu - mu).max(initial=0) / sd.max()), float((np.abs(dvar - var) / (var + BN_EPS)).max()))
+        bn_worst = max(bn_worst, e)
+    # gradients on the committed subsample
+    errs, bad = {}, {}
+    for k, v in grads.items():
+        flat = v.reshape(-1).astype(np.float64)
+        ref = g["gsub:" + k].astype(np.float64)
+        got = flat[MG.sub_index(flat.size)]
+        e = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
+        errs[k] = e
+        lim = max(2e-3, 2.0 * float(g["e32sub:" + k]))
+        if e > lim:
+            bad[k] = (e, lim)
+    worst = sorted(errs.items(), key=lambda r: -r[1])[:5]
+    near0 = 0  # device pre-activations within fp32 rounding of the ReLU boundary (flip candidates)
+    for b in m.engine.blocks:
+        bb = A.blocks[b.name]
+        pre = bb.z.double() * bb.scale.double() + bb.shift.double()
+        near0 += int((pre.abs() < 1e-6 * (bb.shift.double().abs().max() + 1)).sum())
+    _log({"test": fixture, "loss": float(res[0]), "loss_ref": float(g["loss"]), "dice": float(res[1]),
+          "bn_stats_worst_rel": bn_worst, "max_grad_rel_l2_sub": worst[0][1], "worst_grads": worst,
+          "max_fp32_oracle_rel_l2": max(float(g["e32:" + k]) for k in grads), "relu_near_ties": near0})
+    assert abs(res[0] - g["loss"]) < 1e-5 and abs(res[1] - g["dice"]) < 1e-5
+    assert bn_worst < 1e-4, bn_worst
+    assert set(k[6:] for k in g if k.startswith("gnorm:")) == set(grads)
+    assert not bad, bad
+    for k, v in g.items():
+        if k.startswith("gnorm:"):
+            hn = float(np.linalg.norm(grads[k[6:]]))
+            assert abs(hn - v) <= 1e-2 * v + 1e-12, (k, hn, float(v))
+        elif k.startswith("new256:"):
+            name = k[7:]
+            got = neww[name].reshape(-1)[:128].astype(np.float64)
+            v = v[:128]
+            tol = 1e-4 * max(np.abs(v).max(), 1e-3)
+            if name not in grads:  # moving statistics
+                assert np.abs(got - v).max() <= tol, name
+                continue
+            gr = g["g128:" + name][:got.size]
+            sure = np.abs(gr) > 1e-4  # see test_train_step_128_batch4
+            assert np.abs(got - v)[sure].max(initial=0.0) <= tol, name
+            w0 = w[name].reshape(-1)[:got.size]
+            gd = grads[name].reshape(-1)[:got.size]
+            own, _, _ = K.adamw_update(w0, gd, np.zeros_like(w0), np.zeros_like(w0), 1, 2e-3, 1e-4)
+            assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name
+    del m
+    torch.cuda.empty_cache()

@@ -34,6 +34,24 @@ SMOOTH = 1e-7       # K.epsilon() (utils/metrics.py:4)
 DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
 
 
+FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools/bench_sepconv.py sweeps)
+RECOMPUTE_Y_COUT = 64      # fused y-recomputing weight gradient for 64-output blocks only (r2 step A/B)
+
+
+def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bool, fuse: str = "auto",
+                     recompute_y: bool = True):
+    """The kernels a conv_block forward runs: (fused, keep_y).  fused: one unet_sepconv_fwd launch
+    (else unet_dwconv3x3_fwd + unet_pointwise_fwd, which always store y); keep_y: the fused launch
+    also stores the depthwise output y for the weight gradients (training blocks whose weight
+    gradients do not recompute it).  Shared by the engine and bench.py's encoder table."""
+    want = fuse == "always" or (fuse == "auto" and h * w >= FUSE_MIN_PIXELS)
+    if not (want and ops.sepconv_supported(view, n, h, w, cout)):
+        return False, training
+    y_recompute = training and recompute_y and cout == RECOMPUTE_Y_COUT and \
+        ops.sepconv_bwd_filter_supported(view, n, h, w, cout)
+    return True, training and not y_recompute
+
+
 def _mix64(*vals: int) -> int:
     z = 0x243F6A8885A308D3
     for v in vals:
@@ -261,15 +279,12 @@ class UNetEngine:
         bb = A.blocks[b.name]
         gamma, beta, mm, mv = self._bn(b.name)
         dk, pk = self._wts(b)
-        fuse = self.fuse_sepconv == "always" or (self.fuse_sepconv == "auto" and h * w >= 64 * 64)
-        if fuse and ops.sepconv_supported(view, n, h, w, b.cout):
+        fused, keep_y = block_fwd_choice(view, n, h, w, b.cout, training, self.fuse_sepconv, self.recompute_y)
+        if fused:
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view
             stats = training and self.use_bn
-            # (64-output blocks only: the 128-output kernel measured -1.3 % img/s at the 128 x 128 level)
-            bb.y_recompute = training and self.recompute_y and b.cout == 64 and \
-                ops.sepconv_bwd_filter_supported(view, n, h, w, b.cout)
-            keep_y = training and not bb.y_recompute
+            bb.y_recompute = training and not keep_y
             ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
                             bb.part if stats else None)
             if stats:

@@ -82,31 +82,48 @@ class _Workspace:
 WORKSPACE = _Workspace()
 
 
+PEAK_FP32_FLOPS = 157.3e12  # MI355X dense FP32 (matrix = vector rate), MI355X_MICROARCH.md
+PEAK_HBM_BYTES = 8.0e12
+
+
 class KernelTimer:
     """Brackets selected C-ABI ops with HIP events on the stream they are launched on
     (torch's current stream) and accumulates their algorithmic flops / bytes, so a bench
-    can report achieved throughput of one kernel over a timed region."""
+    can report achieved throughput of one kernel over a timed region.  Each record also carries
+    the op's route (which kernels the call launches, e.g. the 1024-channel data gradients' dz
+    pass + plain GEMM), so PMC kernel counts can be matched to the same launch set."""
 
     def __init__(self, names=None):
         self.names = None if names is None else set(names)  # None: every op
-        self.records = []  # (name, flops, bytes, start_event, end_event)
+        self.records = []  # (name, route, flops, bytes, start_event, end_event)
 
     def summary(self):
+        """Per op: launches, ms, flops, bytes, t_roof_ms = sum over launches of
+        max(flops / peak_fp32, bytes / peak_hbm) (each launch against its own bound), and the
+        same per route."""
         torch.cuda.synchronize()
         out = {}
-        for name, fl, nb, e0, e1 in self.records:
-            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
-            d["launches"] += 1
-            d["ms"] += e0.elapsed_time(e1)
-            d["flops"] += fl
-            d["bytes"] += nb
+        for name, route, fl, nb, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            tr = max(fl / PEAK_FP32_FLOPS, nb / PEAK_HBM_BYTES) * 1e3
+            for d in (out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "t_roof_ms": 0.0,
+                                            "hbm_bound_launches": 0, "routes": {}}),):
+                for dd in (d, d["routes"].setdefault(route, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0,
+                                                              "t_roof_ms": 0.0})):
+                    dd["launches"] += 1
+                    dd["ms"] += ms
+                    dd["flops"] += fl
+                    dd["bytes"] += nb
+                    dd["t_roof_ms"] += tr
+                if nb / PEAK_HBM_BYTES > fl / PEAK_FP32_FLOPS:
+                    d["hbm_bound_launches"] += 1
         return out
 
 
 TIMER: Optional[KernelTimer] = None
 
 
-def _call(name: str, work, *args):
+def _call(name: str, work, *args, route: str = "main"):
     """L.call, bracketed by HIP events when TIMER selects `name`; work = (flops, bytes)."""
     t = TIMER
     if t is None or (t.names is not None and name not in t.names):
@@ -117,7 +134,7 @@ def _call(name: str, work, *args):
     e0.record()
     L.call(name, *args)
     e1.record()
-    t.records.append((name, float(work[0]), float(work[1]), e0, e1))
+    t.records.append((name, route, float(work[0]), float(work[1]), e0, e1))
 
 
 def _ws(nbytes: int, device):
@@ -429,10 +446,13 @@ def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int
     _check(dy, "dy", m * cin)
     if dz is not None:
         _check(dz, "dz", m * cout)
+    # (measurement label only) the library forms dz in a streaming pass and runs the plain GEMM
+    # when either side has >= 1024 channels (gemm.hip, unet_pointwise_bwd_data_bnrelu)
+    route = "dz_pass+gemm" if dz is not None and (cin >= 1024 or cout >= 1024) else "gemm_bnbwd"
     _call("unet_pointwise_bwd_data_bnrelu",
           (2.0 * m * cin * cout, 4.0 * (2 * m * cout + m * cin + cin * cout) + (4.0 * m * cout if dz is not None else 0)),
           _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), float(drop_rate),
-          int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream())
+          int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream(), route=route)
 
 
 def pointwise_bwd_data_bnrelu_wgrad(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
