@@ -210,22 +210,28 @@ def synthetic_batch(n, h, w, ncls, seed, device):
     return torch.from_numpy(x).to(device), torch.from_numpy(y).to(device)
 
 
-def cpu_baseline(size, ncls, batch):
-    """SURVEY.md 8(d)'s TF-CPU proxy: the torch-CPU (oneDNN, channels_last, float32) restatement
-    of the identical train step (oracle/torch_ref.py: forward, dice_loss, backward, Keras AdamW,
-    MeanIoU update) on the host cores, a bounded sample of the same workload (>= 10 s)."""
-    from oracle.torch_ref import cpu_info, time_train_steps
+def cpu_baseline(size, ncls, batch, warmup=10, steps=10, threads=0):
+    """SURVEY.md 8(d) / BASELINE.md section 3's TF-CPU proxy: the torch-CPU (oneDNN, channels_last,
+    float32) restatement of the identical train step (oracle/torch_ref.py: forward, dice_loss,
+    backward, Keras AdamW, MeanIoU update) on the host cores -- `warmup` untimed steps, img/s from
+    the median of `steps` timed steps, threads = the machine's physical cores capped by this
+    process's CPU affinity / cgroup quota (oracle/torch_ref.py baseline_threads)."""
+    from oracle.torch_ref import baseline_threads, cpu_info, time_train_steps
     from unet_amd.params import init_weights, unet_variables
-    w = init_weights(unet_variables(3, ncls), 2301)
-    r = time_train_steps(w, size, batch, ncls, min_seconds=10.0, max_steps=4)
     info = cpu_info()
+    nt = threads or baseline_threads(info)
+    w = init_weights(unet_variables(3, ncls), 2301)
+    r = time_train_steps(w, size, batch, ncls, warmup=warmup, steps=steps, threads=nt)
     return {"value": r["value"], "unit": "images/sec", "cores": r["threads"], "kind": "port",
+            "label": "TF-CPU proxy",
             "impl": "torch-CPU restatement of the TF-CPU reference path (oneDNN, channels_last, fp32)",
             "cpu_model": info["cpu_model"], "machine_physical_cores": info["machine_physical_cores"],
-            "affinity_cpus": info["affinity_cpus"],
-            "sample": f"{r['steps']} train steps of batch {batch} at {size}x{size}x3 after 1 warm-up step "
-                      f"({r['seconds']} s; forward + dice_loss + backward + AdamW + MeanIoU update), "
-                      f"{r['threads']} threads"}
+            "machine_logical_cpus": info["machine_logical_cpus"], "affinity_cpus": info["affinity_cpus"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"],
+            "sample": f"median of {r['steps']} timed train steps (each {batch} x {size}x{size}x3; forward + "
+                      f"dice_loss + backward + AdamW + MeanIoU update) after {r['warmup']} warm-up steps; "
+                      f"{r['threads']} threads; median {r['median_step_s']} s/step (min {r['min_step_s']}, "
+                      f"max {r['max_step_s']})"}
 
 
 def spawn_ranks(n: int) -> int:
@@ -252,6 +258,9 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--num-classes", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-warmup", type=int, default=10, help="CPU baseline warm-up steps (BASELINE.md 3)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline timed steps (median reported)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: physical cores, capped)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
@@ -374,7 +383,8 @@ def main():
             torch.cuda.empty_cache()
             out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes, args.batch)
+            out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes, args.batch, args.cpu_warmup,
+                                               args.cpu_steps, args.cpu_threads)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -140,14 +140,34 @@ def cpu_info() -> Dict[str, object]:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         affinity = os.cpu_count() or 1
+    quota = None  # cgroup v2 CPU quota of this process (cpu.max "quota period"), in CPUs
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "machine_physical_cores": len(phys) or None, "affinity_cpus": affinity,
-            "machine_logical_cpus": os.cpu_count()}
+            "machine_logical_cpus": os.cpu_count(), "cgroup_cpu_quota": quota}
 
 
-def time_train_steps(weights, size: int, batch: int, num_classes: int = 1, min_seconds: float = 10.0,
-                     max_steps: int = 4, threads: int = 0) -> Dict[str, object]:
-    """Warm up one step, then time train steps of `batch` synthetic images until `min_seconds`
-    have passed (at most `max_steps`).  Returns img/s and what was run."""
+def baseline_threads(info: Dict[str, object]) -> int:
+    """Threads for the CPU baseline: the machine's physical cores, capped
+    by what this process may actually run on (CPU affinity and the cgroup CPU quota)."""
+    n = info.get("machine_physical_cores") or info.get("affinity_cpus") or 1
+    n = min(int(n), int(info.get("affinity_cpus") or n))
+    q = info.get("cgroup_cpu_quota")
+    if q:
+        n = min(n, max(1, int(q)))
+    return max(1, n)
+
+
+def time_train_steps(weights, size: int, batch: int, num_classes: int = 1, warmup: int = 10, steps: int = 10,
+                     threads: int = 0, max_seconds: float = 300.0) -> Dict[str, object]:
+    """BASELINE.md section 3 protocol: `warmup` untimed train steps, then `steps` timed steps
+    of `batch` synthetic images, each timed alone; img/s from the MEDIAN step (the time budget
+    max_seconds ends the timed steps early, never before 3).  Returns img/s and what was run."""
     if threads > 0:
         torch.set_num_threads(threads)
     used = torch.get_num_threads()
@@ -164,12 +184,19 @@ def time_train_steps(weights, size: int, batch: int, num_classes: int = 1, min_s
         y = np.eye(num_classes, dtype=np.float32)[rng.integers(0, num_classes, (batch, size, size))]
     y = torch.from_numpy(y)
     net = TorchCPUUNet(weights, num_classes)
-    net.train_step(x, y)  # warm-up (oneDNN primitive creation)
-    steps, t0 = 0, time.perf_counter()
-    while steps < max_steps:
+    t_start = time.perf_counter()
+    for _ in range(max(1, warmup)):  # (the first builds the oneDNN primitives)
         net.train_step(x, y)
-        steps += 1
-        if time.perf_counter() - t0 >= min_seconds:
+    t_warm = time.perf_counter() - t_start
+    times = []
+    t0 = time.perf_counter()
+    while len(times) < steps:
+        t = time.perf_counter()
+        net.train_step(x, y)
+        times.append(time.perf_counter() - t)
+        if len(times) >= 3 and time.perf_counter() - t0 > max_seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 3), "steps": steps, "seconds": round(dt, 2), "threads": used}
+    med = float(np.median(times))
+    return {"value": round(batch / med, 3), "steps": len(times), "warmup": max(1, warmup),
+            "median_step_s": round(med, 4), "min_step_s": round(min(times), 4), "max_step_s": round(max(times), 4),
+            "warmup_seconds": round(t_warm, 2), "seconds": round(sum(times), 2), "threads": used}

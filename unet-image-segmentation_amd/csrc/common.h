@@ -50,6 +50,47 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// ------------------------------------------------ fp32 as three bf16 (split-precision GEMMs) ----
+// x == hi + mid + lo EXACTLY for every finite normal fp32 x: hi = RNE_bf16(x), mid = RNE_bf16(x - hi),
+// lo = x - hi - mid (both differences are exact in fp32 and lo has at most 8 significant bits).
+// A GEMM then sums the six products hi.hi + hi.mid + mid.hi + hi.lo + lo.hi + mid.mid on the bf16
+// MFMA (each product exact in its fp32 accumulator); the dropped mid.lo, lo.mid, lo.lo terms are
+// ~2^-23 of |a b|, below the fp32 accumulation's own rounding.  See DESIGN.md "bf16x6".
+typedef short bf16x8 __attribute__((ext_vector_type(8)));  // a 32x32x16 bf16 MFMA operand (4 VGPRs)
+__device__ __forceinline__ unsigned bf16_bits(float x) {
+    return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x);
+}
+__device__ __forceinline__ float bf16_val(unsigned b) { return __uint_as_float(b << 16); }
+struct Split4 {
+    uint2 h, m, l;  // 4 bf16 each, element j in bits 16 (j & 1) of word j >> 1
+};
+__device__ __forceinline__ Split4 split4(float4 v) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[j] = bf16_bits(x[j]);
+        const float r = x[j] - bf16_val(h[j]);
+        m[j] = bf16_bits(r);
+        l[j] = bf16_bits(r - bf16_val(m[j]));
+    }
+    Split4 s;
+    s.h = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    s.m = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+    s.l = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+    return s;
+}
+// acc += a.b over the six significant products of the split operands (a[0..2] = hi, mid, lo)
+__device__ __forceinline__ floatx16 mfma_x6(const bf16x8* a, const bf16x8* b, floatx16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+    return acc;
+}
+
 // Wave issue priority of the critical-path (main-stream) backward kernels: while the weight
 // gradients run beside them on a second stream, their waves win the SIMD's instruction
 // arbitration (s_setprio; 0 = equal priority).  Build-time choice (UNET_MAIN_PRIO); 3 measured

@@ -434,19 +434,33 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
 // As[m][BK+4], Bs[n][BK+4] (k contiguous).  In a group of 8 k, MFMA step s takes k-slot 0 =
 // k0+s and k-slot 1 = k0+4+s, so lane (row, half) feeds 4 consecutive MFMAs from ONE
 // ds_read_b128 of its row.  Row stride BK+4 floats makes those reads conflict-free.
-template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC>
+//
+// X6 (split precision, see common.h split4 / mfma_x6): the staged A and B values are split into
+// three bf16 planes each as they are written to LDS ([row][k] images, k contiguous, row stride
+// BK + 8 bf16 = conflict-free ds_read_b128), and every 16-deep k step runs the six
+// v_mfma_f32_32x32x16_bf16 of mfma_x6 per 32x32 tile: 6 x 32 cycles instead of the 8 x 64 of
+// v_mfma_f32_32x32x2_f32, at fp32 accuracy.  Loads, operand views and epilogues are shared.
+template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC, bool X6 = false>
 __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     main_stream_prio();
     constexpr int LR = BK + 4;     // A (and k-contiguous B) LDS row stride, floats
     constexpr int LB = BN + 4;     // k-major B LDS row stride (n-contiguous weights)
+    constexpr int XR = BK + 8;     // X6: bf16 row stride of the split planes
     constexpr int KQ = BK / 4;
     constexpr int NQ = BN / 4;
     constexpr int AQ = BM * KQ / 256;
     constexpr int BQ = BN * KQ / 256;
     constexpr int TM = BM / 64, TN = BN / 64;
     constexpr int BSZ = BKC ? BN * LR : BK * LB;
-    __shared__ __attribute__((aligned(16))) float As[2][BM * LR];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BSZ];
+    constexpr int F32_BYTES = 4 * 2 * (BM * LR + BSZ);
+    constexpr int X6_BYTES = 2 * 2 * 3 * (BM + BN) * XR;
+    __shared__ __attribute__((aligned(16))) char smem[X6 ? X6_BYTES : F32_BYTES];
+    // fp32 images (the X6 path uses the first bytes of As as epilogue scratch only)
+    float (*As)[BM * LR] = reinterpret_cast<float (*)[BM * LR]>(smem);
+    float (*Bs)[BSZ] = reinterpret_cast<float (*)[BSZ]>(smem + 4 * 2 * BM * LR);
+    // X6 planes: Ax[(buf * 3 + plane) * BM + row][k], Bx[(buf * 3 + plane) * BN + col][k]
+    unsigned short* Ax = reinterpret_cast<unsigned short*>(smem);
+    unsigned short* Bx = Ax + 2 * 3 * BM * XR;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -556,15 +570,44 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             if constexpr (AMODE == A_BNBWD) {
                 if (g.side && blockIdx.y == 0 && kv && aoff[r] >= 0) st4(g.side + aoff[r] + ak, v);
             }
-            *reinterpret_cast<float4*>(&As[buf][(arow + (256 / KQ) * r) * LR + 4 * kq]) = v;
+            const int row = arow + (256 / KQ) * r;
+            if constexpr (X6) {
+                const Split4 sp = split4(v);
+                unsigned short* d = Ax + (buf * 3 * BM + row) * XR + 4 * kq;
+                *reinterpret_cast<uint2*>(d) = sp.h;
+                *reinterpret_cast<uint2*>(d + BM * XR) = sp.m;
+                *reinterpret_cast<uint2*>(d + 2 * BM * XR) = sp.l;
+            } else {
+                *reinterpret_cast<float4*>(&As[buf][row * LR + 4 * kq]) = v;
+            }
         }
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const float4 v = bok[r] ? rb[r] : f4(0.f);
-            if constexpr (BKC)
+            if constexpr (X6) {
+                const Split4 sp = split4(v);
+                if constexpr (BKC) {  // 4 consecutive k of one column
+                    unsigned short* d = Bx + (buf * 3 * BN + bq_n + (256 / KQ) * r) * XR + 4 * bq_k;
+                    *reinterpret_cast<uint2*>(d) = sp.h;
+                    *reinterpret_cast<uint2*>(d + BN * XR) = sp.m;
+                    *reinterpret_cast<uint2*>(d + 2 * BN * XR) = sp.l;
+                } else {  // 4 consecutive columns of one k: transposed into the [col][k] image
+                    unsigned short* d = Bx + (buf * 3 * BN + 4 * bq_n) * XR + bq_k + (256 / NQ) * r;
+                    const unsigned hw[4] = {sp.h.x & 0xFFFFu, sp.h.x >> 16, sp.h.y & 0xFFFFu, sp.h.y >> 16};
+                    const unsigned mw[4] = {sp.m.x & 0xFFFFu, sp.m.x >> 16, sp.m.y & 0xFFFFu, sp.m.y >> 16};
+                    const unsigned lw[4] = {sp.l.x & 0xFFFFu, sp.l.x >> 16, sp.l.y & 0xFFFFu, sp.l.y >> 16};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        d[j * XR] = (unsigned short)hw[j];
+                        d[BN * XR + j * XR] = (unsigned short)mw[j];
+                        d[2 * BN * XR + j * XR] = (unsigned short)lw[j];
+                    }
+                }
+            } else if constexpr (BKC) {
                 *reinterpret_cast<float4*>(&Bs[buf][(bq_n + (256 / KQ) * r) * LR + 4 * bq_k]) = v;
-            else
+            } else {
                 *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = v;
+            }
         }
     };
 
@@ -583,6 +626,27 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load_stage((kt + 1) * BK);
+        if constexpr (X6) {
+#pragma unroll
+            for (int ks = 0; ks < BK / 16; ++ks) {
+                bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+                        af[tm][p] = *reinterpret_cast<const bf16x8*>(
+                            Ax + ((buf * 3 + p) * BM + wm * (BM / 2) + tm * 32 + lo) * XR + ks * 16 + 8 * hi);
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        bfr[tn][p] = *reinterpret_cast<const bf16x8*>(
+                            Bx + ((buf * 3 + p) * BN + wn * (BN / 2) + tn * 32 + lo) * XR + ks * 16 + 8 * hi);
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af[tm], bfr[tn], acc[tm][tn]);
+            }
+        } else {
 #pragma unroll
         for (int kg = 0; kg < BK / 8; ++kg) {
             float4 af[TM], bf[TN];
@@ -608,6 +672,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                     acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].z, bf[tn].z, acc[tm][tn], 0, 0, 0);
                     acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm].w, bf[tn].w, acc[tm][tn], 0, 0, 0);
                 }
+        }
         }
         if (kt + 1 < nk) store_stage(buf ^ 1);
         __syncthreads();
@@ -1093,17 +1158,26 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
-template <int BN, int BKk, int AMODE, bool DROP, int EPI>
+template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false>
 void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
     dim3 grid((unsigned)cdiv(a.M, 128), (unsigned)cdiv(a.N, BN));
-    if (a.sbk == 1) gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, true><<<grid, 256, 0, st>>>(a);
-    else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false><<<grid, 256, 0, st>>>(a);
+    if (a.sbk == 1) gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
+    else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
 }
+
+// Split-precision (bf16x6) rows GEMM: 128 x 128 tiles, BK 16 or 32 (lab A/B: UNET_X6)
+bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
 
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     if (rows_vec_ok(a, AMODE)) {
         const RowsCfg c = rows_cfg(a, AMODE);
+        if (rows_x6()) {
+            if (c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI, true>(a, st);
+            else launch_rows_tile<128, 16, AMODE, DROP, EPI, true>(a, st);
+            UNET_CHECK_LAUNCH(what);
+            return 0;
+        }
         if (c.bn == 64 && c.bk == 16) launch_rows_tile<64, 16, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 64 && c.bk == 32) launch_rows_tile<64, 32, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 128 && c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI>(a, st);
