@@ -55,18 +55,28 @@ def _list(d):
     return sorted(f for f in os.listdir(d) if f.lower().endswith(IMG_EXT))
 
 
-def load_image(path, size, mode):
+def load_image_u8(path, size, mode):
+    """Decoded + resized image as uint8 HWC (bilinear for RGB frames, nearest for masks)."""
     from PIL import Image
     im = Image.open(path).convert("RGB" if mode == "rgb" else "L")
     if im.size != (size[1], size[0]):
         im = im.resize((size[1], size[0]), Image.BILINEAR if mode == "rgb" else Image.NEAREST)
-    a = np.asarray(im, dtype=np.float32) / 255.0
+    a = np.asarray(im, dtype=np.uint8)
     return a if a.ndim == 3 else a[..., None]
 
 
+def load_image(path, size, mode):
+    return load_image_u8(path, size, mode).astype(np.float32) / 255.0
+
+
 class PairLoader:
+    """cache_bytes: decoded, resized samples are kept as uint8 (256 x 256 x 4 B = 256 KiB per
+    pair at 256 x 256) up to this budget, so PNG decoding (~25 ms per 960 x 540 frame on one
+    core, tools/bench_loader.py) is paid once per file, not once per epoch: the decode and resize
+    are deterministic, so the batches are identical to decoding every epoch."""
+
     def __init__(self, frames_dir, masks_dir, size, batch_size, seed, shuffle=True, horizontal_flip=False, rank=0,
-                 world=1, workers=4):
+                 world=1, workers=8, cache_bytes=16 << 30):
         if batch_size < world:
             raise ValueError(f"batch size {batch_size} < {world} data-parallel ranks: every rank needs a sample")
         self.frames = [os.path.join(frames_dir, f) for f in _list(frames_dir)]
@@ -78,6 +88,9 @@ class PairLoader:
         self.samples = len(self.frames)
         self.workers = max(1, int(workers))
         self._pool = None
+        self.cache_bytes = int(cache_bytes)
+        self._cache = {}
+        self._cached_bytes = 0
 
     def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
         epoch = 0
@@ -92,8 +105,15 @@ class PairLoader:
             epoch += 1
 
     def _sample(self, i, flip):
-        x = load_image(self.frames[i], self.size, "rgb")
-        y = load_image(self.masks[i], self.size, "grayscale")
+        xy = self._cache.get(i)
+        if xy is None:
+            xy = (load_image_u8(self.frames[i], self.size, "rgb"), load_image_u8(self.masks[i], self.size, "grayscale"))
+            nb = xy[0].nbytes + xy[1].nbytes
+            if self._cached_bytes + nb <= self.cache_bytes:
+                self._cache[i] = xy  # (dict item assignment is atomic under the GIL)
+                self._cached_bytes += nb
+        x = xy[0].astype(np.float32) / 255.0  # rescale=1/255 (reference scripts/train.py:170-178)
+        y = xy[1].astype(np.float32) / 255.0
         if flip:
             x, y = x[:, ::-1], y[:, ::-1]
         return x, y
