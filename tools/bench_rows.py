@@ -95,6 +95,16 @@ def main():
         err = rel(out, ref)
         tot.setdefault("convT_fwd", []).append(emit("convT_fwd", name, m, cin, 4 * cout, s, 8.0 * m * cin * cout, err))
         del x, out
+    for name, hw, cin, cout in DGRAD:  # pointwise weight gradient dW = y^T dz
+        m = B * hw * hw
+        y = torch.randn(m, cin, generator=g).to(dev)
+        dz = torch.randn(m, cout, generator=g).to(dev)
+        dpk = torch.empty(cin, cout, device=dev)
+        s = bench(lambda: ops.pointwise_bwd_filter(y, dz, m, cin, cout, dpk))
+        err = rel(dpk, y.double().T @ dz.double())
+        tot.setdefault("pointwise_wgrad", []).append(emit("pointwise_wgrad", name, m, m, cin * cout, s,
+                                                           2.0 * m * cin * cout, err))
+        del y, dz
     for kind, ts in tot.items():
         us = sum(t[0] for t in ts) * 1e6
         fl = sum(t[1] for t in ts)

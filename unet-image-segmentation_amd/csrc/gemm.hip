@@ -831,15 +831,28 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 }
 
 // ------------------------------------------------------------- vectorised wgrad GEMM ----
-template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
+// X6 (split precision, 128 x 128 tiles): the reduction runs over pixels m, which both operands
+// hold m-major, so the bf16 planes are written transposed, [channel][m] with a 40-byte row (16 m +
+// 4 pad): threads 0-127 stage A, 128-255 B, each 4 consecutive m of one channel quad (lane
+// (quad, m-quad) = (u / 4, u % 4)): after an in-register 4 x 4 transpose every channel's 4 m go out
+// as one 8-byte store per plane, conflict-free at that row stride, and the MFMA fragments (8 m of
+// a channel) come back as two conflict-free ds_read_b64 (the 40-byte rows are not 16-byte aligned).
+template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP, bool X6 = false>
 __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
+    static_assert(!X6 || (BP == 128 && BQ == 128), "X6 wgrad: 128 x 128 tiles");
     constexpr int LDA = BP + 4, LDB = BQ + 4;
     constexpr int TM = BP / 64, TN = BQ / 64;
     constexpr int PQ = BP / 4, QQ = BQ / 4;          // quads per m-row
-    constexpr int AR = BK * PQ / 256, BR = BK * QQ / 256;
-    constexpr int AS = 256 / PQ, BS = 256 / QQ;      // m-row step between a thread's quads
-    __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
+    constexpr int AR = X6 ? 4 : BK * PQ / 256, BR = X6 ? 4 : BK * QQ / 256;
+    constexpr int AS = X6 ? 1 : 256 / PQ, BS = X6 ? 1 : 256 / QQ;  // m-row step between a thread's quads
+    constexpr int XW = 20;                           // X6 plane row stride (bf16): 16 m + 4 pad
+    constexpr int F32_BYTES = 4 * 2 * BK * (LDA + LDB);
+    constexpr int X6_BYTES = 2 * 2 * 3 * (BP + BQ) * XW;
+    __shared__ __attribute__((aligned(16))) char smem[X6 ? X6_BYTES : F32_BYTES];
+    float (*As)[BK * LDA] = reinterpret_cast<float (*)[BK * LDA]>(smem);
+    float (*Bs)[BK * LDB] = reinterpret_cast<float (*)[BK * LDB]>(smem + 4 * 2 * BK * LDA);
+    unsigned short* Ax = reinterpret_cast<unsigned short*>(smem);  // [(buf * 3 + plane) * BP + p][m]
+    unsigned short* Bx = Ax + 2 * 3 * BP * XW;                     // [(buf * 3 + plane) * BQ + q][m]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wp = wave >> 1, wq = wave & 1;
@@ -849,8 +862,10 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     const int q0 = (blockIdx.x / ntp) * BQ;
     const int mb = (int)(blockIdx.y * g.mslice);
     const int me = (int)((mb + g.mslice) < g.M ? (mb + g.mslice) : g.M);
+    const bool roleA = !X6 || tid < 128, roleB = !X6 || tid >= 128;
+    const int unit = tid & 127;
 
-    const int apq = tid % PQ, amm = tid / PQ;
+    const int apq = X6 ? unit >> 2 : tid % PQ, amm = X6 ? 4 * (unit & 3) : tid / PQ;
     const int p = p0 + 4 * apq;
     const bool pv = p < g.P;
     float4 asc = f4(1.f), ash = f4(0.f);
@@ -866,7 +881,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         const int co = p - ab * g.uf;
         poff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
     }
-    const int bqq = tid % QQ, bmm = tid / QQ;
+    const int bqq = X6 ? unit >> 2 : tid % QQ, bmm = X6 ? 4 * (unit & 3) : tid / QQ;
     const int q = q0 + 4 * bqq;
     const bool qv = q < g.Q;
     float4 bsc = f4(1.f), bsh = f4(0.f), bmu = f4(0.f), bp_ = f4(0.f), bq_ = f4(0.f);
@@ -902,7 +917,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         for (int r = 0; r < AR; ++r) {
             const int m = k0 + amm + AS * r;
             float4 v = f4(0.f);
-            if (pv && m < me) {
+            if (roleA && pv && m < me) {
                 if constexpr (AMODE == W_UNSHUFFLE) {
                     v = ld4(g.a.src0 + (4 * ur[r] * g.uW + 2 * uj[r]) * g.uf + poff);
                 } else {
@@ -920,7 +935,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         for (int r = 0; r < BR; ++r) {
             const int m = k0 + bmm + BS * r;
             float4 v = f4(0.f);
-            if (qv && m < me) {
+            if (roleB && qv && m < me) {
                 v = ld4(g.b.src0 + (int64_t)m * g.b.c0 + q);
                 if constexpr (BMODE == W_BNRELU) v = bnrelu4(v, bsc, bsh);
                 if constexpr (BMODE == W_BNBWD) {
@@ -954,15 +969,35 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     };
     const bool csum_on = g.colpart != nullptr && (int)blockIdx.x < ntp;  // q-tile 0 blocks sum A's columns
     float4 csum = f4(0.f);
-    auto store_stage = [&](int buf) {
+    // X6: 4 consecutive m (rows r = 0..3) of channel c of the thread's quad, split, into the planes
+    auto store_t4 = [&](unsigned short* base, int rows, const float4* rv) {
+        const float4 cols[4] = {make_float4(rv[0].x, rv[1].x, rv[2].x, rv[3].x),
+                                make_float4(rv[0].y, rv[1].y, rv[2].y, rv[3].y),
+                                make_float4(rv[0].z, rv[1].z, rv[2].z, rv[3].z),
+                                make_float4(rv[0].w, rv[1].w, rv[2].w, rv[3].w)};
 #pragma unroll
-        for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[buf][(amm + AS * r) * LDA + 4 * apq]) = ra[r];
-        if (csum_on) {
+        for (int c = 0; c < 4; ++c) {
+            const Split4 sp = split4(cols[c]);
+            unsigned short* d = base + c * XW;
+            *reinterpret_cast<uint2*>(d) = sp.h;
+            *reinterpret_cast<uint2*>(d + rows * XW) = sp.m;
+            *reinterpret_cast<uint2*>(d + 2 * rows * XW) = sp.l;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        if constexpr (X6) {
+            if (roleA) store_t4(Ax + (buf * 3 * BP + 4 * apq) * XW + amm, BP, ra);
+            else store_t4(Bx + (buf * 3 * BQ + 4 * bqq) * XW + bmm, BQ, rb);
+        } else {
+#pragma unroll
+            for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[buf][(amm + AS * r) * LDA + 4 * apq]) = ra[r];
+#pragma unroll
+            for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[buf][(bmm + BS * r) * LDB + 4 * bqq]) = rb[r];
+        }
+        if (csum_on && roleA) {
 #pragma unroll
             for (int r = 0; r < AR; ++r) csum = add4(csum, ra[r]);
         }
-#pragma unroll
-        for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[buf][(bmm + BS * r) * LDB + 4 * bqq]) = rb[r];
     };
 
     floatx16 acc[TM][TN];
@@ -982,6 +1017,30 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load_stage(mb + (kt + 1) * BK);
+        if constexpr (X6) {
+            bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const unsigned short* a =
+                        Ax + ((buf * 3 + pl) * BP + wp * (BP / 2) + tm * 32 + lo) * XW + 8 * hi;
+                    const uint2 u0 = *reinterpret_cast<const uint2*>(a), u1 = *reinterpret_cast<const uint2*>(a + 4);
+                    af[tm][pl] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const unsigned short* b =
+                        Bx + ((buf * 3 + pl) * BQ + wq * (BQ / 2) + tn * 32 + lo) * XW + 8 * hi;
+                    const uint2 u0 = *reinterpret_cast<const uint2*>(b), u1 = *reinterpret_cast<const uint2*>(b + 4);
+                    bfr[tn][pl] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                }
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af[tm], bfr[tn], acc[tm][tn]);
+        } else {
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
             float av[TM], bv[TN];
@@ -995,14 +1054,21 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
                 for (int tn = 0; tn < TN; ++tn)
                     acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
         }
+        }
         if (kt + 1 < nk) store_stage(buf ^ 1);
         __syncthreads();
     }
-    if (csum_on) {  // fixed-order sum over the AS m-rows of each column quad (the loop ended on a barrier)
+    if (csum_on) {  // fixed-order sum over the m-rows of each column quad (the loop ended on a barrier)
         float4* T = reinterpret_cast<float4*>(&As[0][0]);
         T[tid] = csum;
         __syncthreads();
-        if (tid < PQ && pv) {
+        if constexpr (X6) {  // thread u < 128 holds quad u / 4, m-quad u % 4
+            if (tid < PQ && p0 + 4 * tid < g.P) {
+                float4 t = T[4 * tid];
+                for (int j = 1; j < 4; ++j) t = add4(t, T[4 * tid + j]);
+                st4(g.colpart + (int64_t)blockIdx.y * g.P + p0 + 4 * tid, t);
+            }
+        } else if (tid < PQ && pv) {
             float4 t = T[tid];
             for (int j = 1; j < AS; ++j) t = add4(t, T[j * PQ + tid]);
             st4(g.colpart + (int64_t)blockIdx.y * g.P + p, t);
@@ -1223,6 +1289,8 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     return w;
 }
 
+bool wgrad_x6() { return lab_knob("UNET_X6", 0) != 0; }
+
 template <int AMODE, bool ADROP, int BMODE, bool BDROP>
 void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
     dim3 grid((unsigned)w.tiles, (unsigned)w.S);
@@ -1230,7 +1298,9 @@ void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
                      (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
                      ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
     if (vec || BMODE == W_BNBWD) {
-        if (w.bp == 128 && w.bq == 128)
+        if (w.bp == 128 && w.bq == 128 && wgrad_x6())
+            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP, true><<<grid, 256, 0, st>>>(a);
+        else if (w.bp == 128 && w.bq == 128)
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
         else if (w.bp == 128)
             gemm_wgrad_vec<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
