@@ -30,7 +30,7 @@ CONVT = [("dec4_upsample", 16, 1024, 512), ("dec3_upsample", 32, 512, 256), ("de
          ("dec1_upsample", 128, 128, 64)]
 
 
-def bench(fn, iters=20):
+def bench(fn, iters=int(os.environ.get("ITERS", 20))):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
