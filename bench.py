@@ -96,7 +96,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
     of 3 groups), against
     t_roof = max(flops / peak_fp32, bytes / peak_hbm) with flops = px(18 Cin + 2 Cin Cout) and
     bytes = 4 (px (Cin + Cout) + 9 Cin + Cin Cout + 4 Cout).  Runs the train step's own kernel
-    choice per block (engine.block_fwd_choice: the same launches, y stores included)."""
+    choice per block (engine.block_fwd_choice: the same launches, y stores included; block2 also
+    writes the next stage's 2x2 pooling selection, which the pooled block1 reads)."""
     import torch
     from unet_amd import ops
     from unet_amd.engine import block_fwd_choice
@@ -108,15 +109,16 @@ def encoder_block_roofline(batch, size, device, reps=10):
         for blk, (ci, co) in enumerate(((cin, f), (f, f))):
             pool = lvl > 0 and blk == 0
             hh = h
-            src = torch.rand((batch, 2 * hh if pool else hh, 2 * hh if pool else hh, ci), generator=g).to(device)
+            # a max-pooled input is read as the step reads it: a BN+ReLU view of the previous
+            # block's 2x2 window selections (n, hh, hh, ci), written by that block (below)
+            src = torch.rand((batch, hh, hh, ci), generator=g).to(device)
             sc = torch.rand(ci, generator=g).to(device) + 0.5
             sh = torch.randn(ci, generator=g).to(device) * 0.1
             ck = ci
             if lvl == 0 and blk == 0 and ci % 4:  # the engine zero-pads the image to 4 channels
                 ck = (ci + 3) // 4 * 4
                 src = torch.cat([src, torch.zeros(src.shape[:3] + (ck - ci,), device=device)], dim=3)
-            view = View.plain(src) if (lvl == 0 and blk == 0) else (View.pool_bnrelu(src, sc, sh) if pool
-                                                                     else View.bnrelu(src, sc, sh))
+            view = View.plain(src) if (lvl == 0 and blk == 0) else View.bnrelu(src, sc, sh)
             dk = torch.randn((3, 3, ck, 1), generator=g).to(device)
             pk = (torch.randn((1, 1, ck, co), generator=g) / ci ** 0.5).to(device)
             m = batch * hh * hh
@@ -127,13 +129,18 @@ def encoder_block_roofline(batch, size, device, reps=10):
             ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
             part = torch.zeros(ops.bn_partials_numel(m, co), device=device)
+            # block2 of each stage also writes the pooling selection of z for the next stage
+            zsel = torch.empty((batch, hh // 2, hh // 2, co), device=device) if blk == 1 else None
+            gam = (torch.rand(co, generator=g) - 0.3).to(device) if blk == 1 else None
 
             def run():
                 if fused:
-                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf if keep_y else None, z, part)
+                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf if keep_y else None, z, part, zsel, gam)
                 else:
                     ops.dwconv3x3_fwd(view, batch, hh, hh, dk, ybuf)
                     ops.pointwise_fwd(ybuf, m, ck, co, pk, z, part)
+                    if zsel is not None:
+                        ops.pool_select(z, batch, hh, hh, co, gam, zsel)
             for _ in range(3):
                 run()
             ts = []
@@ -151,7 +158,7 @@ def encoder_block_roofline(batch, size, device, reps=10):
             t_roof = max(fl / (PEAK_FP32_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)) * 1e6
             rows.append({"block": f"enc{lvl + 1}_block{blk + 1}", "hw": hh, "cin": ci, "cout": co,
                          "kernel": ("unet_sepconv_fwd" + (" (+y store)" if keep_y else "") if fused
-                                    else "dwconv3x3_fwd+pointwise_fwd") +
+                                    else "dwconv3x3_fwd+pointwise_fwd") + (" +pool select" if blk == 1 else "") +
                                    (f" (input padded {ci}->{ck} ch)" if ck != ci else ""),
                          "bound": "mfma" if fl / nb >= RIDGE else "hbm", "us": round(us, 1),
                          "t_roof_us": round(t_roof, 1), "frac": round(t_roof / us, 4),

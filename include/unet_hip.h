@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 8
+#define UNET_ABI_VERSION 9
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -156,7 +156,18 @@ int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
 int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int w, int cout);
 int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                      int cout, const float* pw_kernel, float* y, float* z,
-                     float* bn_partials, unet_stream_t stream);
+                     float* bn_partials, float* z_pool_sel, const float* gamma,
+                     unet_stream_t stream);
+/* z_pool_sel (optional, (N, h/2, w/2, cout)): the encoder stage's MaxPooling2D((2,2))
+ * (model/u_net.py:69) prepared for its consumer: per 2x2 window of z and channel, the raw
+ * value the max-pool of relu(z * scale + shift) selects -- the window max where gamma >= 0,
+ * the min where gamma < 0 (gamma = the block's BN gamma; NULL = no BatchNorm: max).  scale has
+ * gamma's sign and fmaf / relu are monotone, so a BNRELU view of z_pool_sel reads exactly the
+ * pooled activation, one value per output pixel instead of four.  Written by the kernel's
+ * epilogue (register-A schedule) or by unet_pool_select after it.  The max-pool BACKWARD still
+ * routes through z (first maximum of the window): POOL_BNRELU views of z.                   */
+int unet_pool_select(const float* z, int n, int h, int w, int c, const float* gamma,
+                     float* out, unet_stream_t stream);
 /* Kernel schedule of unet_sepconv_fwd (process-wide; returns the previous value, < 0 on a bad
  * value).  AUTO: the register-A kernel (each lane computes the depthwise output straight in the
  * MFMA operand layout) for BN+ReLU / concat / plain views of >= 64 channels, the LDS-A-tile

@@ -743,3 +743,48 @@ def test_copy_strided(ops):
     assert torch.equal(pp[:, :, :3], pk) and not pp[:, :, 3].any()
     with pytest.raises(ValueError):
         ops.copy_strided(x, 2 * 8 * 16, 3, 4, xp, 4)  # source too small for its stride
+
+
+def _pool_ref(a):
+    N, H, W, C = a.shape
+    return a.reshape(N, H // 2, 2, W // 2, 2, C).max((2, 4))
+
+
+@pytest.mark.parametrize("n,h,w,c", [(2, 8, 16, 64), (1, 16, 32, 128), (3, 4, 6, 8)])
+def test_pool_select(ops, n, h, w, c):
+    """unet_pool_select: a BN+ReLU view of the selection reads bitwise the 2x2 max-pool of the BN+ReLU
+    view of z (MaxPooling2D, model/u_net.py:69), for gammas of either sign (and +-0) and without BN."""
+    rng = np.random.default_rng(n * h + c)
+    z = f32(rng.standard_normal((n, h, w, c)) * 2)
+    z[0, 0, 0, :4] = z[0, 0, 1, :4]  # ties inside a window
+    gamma = f32(rng.standard_normal(c))
+    gamma[:2] = [0.0, -0.0]
+    rstd = f32(0.5 + rng.random(c))
+    scale, shift = f32(gamma * rstd), f32(rng.standard_normal(c) * 0.3)
+    out = torch.empty((n, h // 2, w // 2, c), device="cuda")
+    for g, sc in ((gamma, scale), (None, np.ones(c, np.float32))):
+        ops.pool_select(dev(z), n, h, w, c, None if g is None else dev(g), out)
+        tz, tsc, tsh = dev(z), dev(sc), dev(shift)
+        got = torch.relu(torch.addcmul(tsh, out, tsc))  # fmaf(sel, sc, sh) as the views evaluate it
+        pre = torch.relu(torch.addcmul(tsh, tz, tsc))
+        ref = pre.reshape(n, h // 2, 2, w // 2, 2, c).amax((2, 4))
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,cout", [(1, 2, 8, 16, 64, 64), (1, 1, 16, 32, 128, 128),
+                                                (1, 1, 8, 32, 64, 192), (2, 2, 8, 16, 64, 128)])
+def test_sepconv_pool_selection_epilogue(ops, sep_schedule, mode, n, h, w, c0, cout):
+    """unet_sepconv_fwd's z_pool_sel (register-A epilogue, or the separate pass after the LDS-A-tile
+    kernel) equals unet_pool_select of its own z, bitwise."""
+    rng = np.random.default_rng(7 + cout)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, 0)
+    dk = dev(f32(rng.standard_normal((3, 3, c0, 1))))
+    pk = dev(f32(rng.standard_normal((1, 1, c0, cout)) / np.sqrt(c0)))
+    v = _mk_view(ops, mode, t)
+    gamma = dev(f32(rng.standard_normal(cout)))
+    z = torch.empty((n, h, w, cout), device="cuda")
+    zsel = torch.full((n, h // 2, w // 2, cout), 7.0, device="cuda")
+    ops.sepconv_fwd(v, n, h, w, dk, cout, pk, None, z, None, zsel, gamma)
+    ref = torch.empty_like(zsel)
+    ops.pool_select(z, n, h, w, cout, gamma, ref)
+    assert torch.equal(zsel, ref)

@@ -21,7 +21,16 @@ struct SepArgs {
     float* y;         // optional (N,H,W,Cin)
     float* z;         // (N,H,W,Cout)
     float2* stats;    // [M/128][Cout]
+    float* zsel;         // optional (N,H/2,W/2,Cout): the 2x2 pooling selection of z (pool_select_kernel)
+    const float* gamma;  // zsel: BN gamma (its sign orders the window), NULL = no BN (max)
 };
+
+// The raw z value of a 2x2 window that the max-pool of relu(z * s + b) takes, with s of the sign of
+// gamma: the max where gamma >= 0 (+0 included), the min where gamma < 0.  fmaf is monotone in z,
+// so relu(fmaf(sel, s, b)) is bitwise the max over the window of relu(fmaf(z, s, b)).
+__device__ __forceinline__ float pool_sel(float a, float b, float c, float d, bool neg) {
+    return neg ? fminf(fminf(a, b), fminf(c, d)) : fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
 
 // register-A schedule (sepconv_rk.hip): returns 0, or -1 if the mode/shape has no such kernel
 int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);

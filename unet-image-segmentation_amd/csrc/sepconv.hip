@@ -393,9 +393,48 @@ extern "C" int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int 
            (int64_t)n * h * w * C * (x->mode == UNET_VIEW_POOL_BNRELU ? 4 : 1) < (int64_t(1) << 31);
 }
 
-extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel, int cout,
-                                const float* pw_kernel, float* y, float* z, float* bn_partials,
+namespace unet {
+namespace {
+// zsel[n][i][j][c] = pool_sel over z's 2x2 window (2i..2i+1, 2j..2j+1), channel quads
+__global__ __launch_bounds__(256) void pool_select_kernel(const float* __restrict__ z, int64_t quads, int H2, int W2,
+                                                          int C, const float* __restrict__ gamma, float* __restrict__ out) {
+    const int C4 = C / 4;
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < quads; e += (int64_t)gridDim.x * 256) {
+        const int q = (int)(e % C4);
+        const int64_t p = e / C4;  // pooled pixel (n, i, j)
+        const int j = (int)(p % W2);
+        const int64_t ni = p / W2;  // n * H2 + i
+        const int64_t r0 = (2 * ni) * (2 * W2) + 2 * j;  // z pixel (n, 2i, 2j): rows of 2 W2 pixels
+        const float* b = z + r0 * C + 4 * q;
+        const float4 a = ld4(b), bb = ld4(b + C), c = ld4(b + 2 * W2 * C), d = ld4(b + 2 * W2 * C + C);
+        const float4 gm = gamma ? ld4(gamma + 4 * q) : f4(0.f);
+        float4 o;
+        o.x = sep::pool_sel(a.x, bb.x, c.x, d.x, signbit(gm.x));
+        o.y = sep::pool_sel(a.y, bb.y, c.y, d.y, signbit(gm.y));
+        o.z = sep::pool_sel(a.z, bb.z, c.z, d.z, signbit(gm.z));
+        o.w = sep::pool_sel(a.w, bb.w, c.w, d.w, signbit(gm.w));
+        st4(out + p * C + 4 * q, o);
+    }
+}
+}  // namespace
+}  // namespace unet
+
+extern "C" int unet_pool_select(const float* z, int n, int h, int w, int c, const float* gamma, float* out,
                                 unet_stream_t stream) {
+    UNET_CHECK_ARG(z && out && n > 0 && h > 0 && w > 0 && c > 0, "unet_pool_select: bad arguments");
+    UNET_CHECK_ARG(h % 2 == 0 && w % 2 == 0 && c % 4 == 0, "unet_pool_select: needs even h, w and c %% 4 == 0");
+    UNET_CHECK_ARG(((uintptr_t)z | (uintptr_t)out | (uintptr_t)gamma) % 16 == 0, "unet_pool_select: 16-B alignment");
+    const int64_t quads = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
+    int64_t blocks = (quads + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    pool_select_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(z, quads, h / 2, w / 2, c, gamma, out);
+    UNET_CHECK_LAUNCH("unet_pool_select");
+    return 0;
+}
+
+extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel, int cout,
+                                const float* pw_kernel, float* y, float* z, float* bn_partials, float* z_pool_sel,
+                                const float* gamma, unet_stream_t stream) {
     if (check_view(x, "unet_sepconv_fwd")) return -1;
     UNET_CHECK_ARG(unet_sepconv_fwd_supported(x, n, h, w, cout),
                    "unet_sepconv_fwd: unsupported shape (needs h%%8==0, w%%16==0, channels%%4==0)");
@@ -414,6 +453,18 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     a.stats = reinterpret_cast<float2*>(bn_partials);
     const bool stats = bn_partials != nullptr, wy = y != nullptr, drop = x->drop_rate > 0.f;
     hipStream_t st = as_stream(stream);
+    if (z_pool_sel) {
+        UNET_CHECK_ARG(h % 2 == 0 && w % 2 == 0 && ((uintptr_t)z_pool_sel | (uintptr_t)gamma) % 16 == 0,
+                       "unet_sepconv_fwd: z_pool_sel needs even h, w and 16-B aligned buffers");
+    }
+    if (z_pool_sel && !(g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout))) {
+        // LDS-A-tile schedule: the selection in a pass over z after the kernel
+        const int rc = unet_sepconv_fwd(x, n, h, w, dw_kernel, cout, pw_kernel, y, z, bn_partials, nullptr, nullptr,
+                                        stream);
+        return rc ? rc : unet_pool_select(z, n, h, w, cout, gamma, z_pool_sel, stream);
+    }
+    a.zsel = z_pool_sel;
+    a.gamma = gamma;
     // register-A schedule where it exists (BN+ReLU / concat / plain views, >= 64 channels) unless
     // the LDS-A-tile schedule is forced; max-pool views keep the LDS-A-tile kernel (4 raw loads
     // per halo element need its wider 8-wave staging)

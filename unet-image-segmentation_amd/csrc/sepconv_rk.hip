@@ -325,6 +325,32 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     }
     // z: the wave's 32 pixels x BN channels as float4s (BN / 4 per pixel, 64 per instruction)
     constexpr int Q4 = BN / 4, NS = 32 * Q4 / 64;
+    if (g.zsel) {
+        // the wave's two pixel rows hold 8 whole 2x2 windows: their pooling selection (zsel) for
+        // the next stage's max-pool view.  T row of pixel (sub, col): col, or 16 + ((col + 2) & 15)
+        // on the second row (rk_col's rotation inverted)
+        constexpr int NP4 = 8 * Q4 / 64;
+#pragma unroll
+        for (int i = 0; i < NP4; ++i) {
+            const int idx = i * 64 + lane, j = idx / Q4, q = idx - j * Q4;
+            const int c0 = 2 * j, c1 = 2 * j + 1;
+            const float4 a = *reinterpret_cast<const float4*>(&T[c0 * TLD + 4 * q]);
+            const float4 b = *reinterpret_cast<const float4*>(&T[c1 * TLD + 4 * q]);
+            const float4 c = *reinterpret_cast<const float4*>(&T[(16 + ((c0 + 2) & 15)) * TLD + 4 * q]);
+            const float4 d = *reinterpret_cast<const float4*>(&T[(16 + ((c1 + 2) & 15)) * TLD + 4 * q]);
+            const int col = n0 + 4 * q;
+            if (col < g.Cout) {
+                const float4 gm = g.gamma ? ld4(g.gamma + col) : f4(0.f);
+                float4 o;
+                o.x = pool_sel(a.x, b.x, c.x, d.x, signbit(gm.x));
+                o.y = pool_sel(a.y, b.y, c.y, d.y, signbit(gm.y));
+                o.z = pool_sel(a.z, b.z, c.z, d.z, signbit(gm.z));
+                o.w = pool_sel(a.w, b.w, c.w, d.w, signbit(gm.w));
+                const int H2 = g.H >> 1, W2 = g.W >> 1;
+                st4(g.zsel + ((int64_t)(n * H2 + (h0 >> 1) + wave) * W2 + (w0 >> 1) + j) * g.Cout + col, o);
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         const int idx = i * 64 + lane, row = idx / Q4, q = idx - row * Q4;

@@ -91,6 +91,7 @@ class BlockBufs:
     bn_slabs: int = 0  # > 0: bnpart holds this many fresh slabs for the next backward of the block
     bnpart_s: int = -1  # the slab count bnpart's counters were last laid out for
     y_recompute: bool = False  # last training forward kept no y: the weight grads recompute it
+    zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
 
 
 @dataclass
@@ -250,6 +251,9 @@ class UNetEngine:
                 mean=torch.zeros(b.cout, **f32), rstd=torch.zeros(b.cout, **f32),
                 scale=torch.zeros(b.cout, **f32), shift=torch.zeros(b.cout, **f32),
                 da=torch.empty((n, h, w, b.cout), **f32))
+        for _, _, b2 in self.enc:  # the pooled stage outputs: their consumers read one value per window
+            h, w = self._dims(b2.level)
+            blocks[b2.name].zsel = torch.empty((n, h // 2, w // 2, b2.cout), **f32)
         up, dup = {}, {}
         for stage, fi, cin, b1, b2 in self.dec:
             h, w = self._dims(b1.level)
@@ -286,7 +290,7 @@ class UNetEngine:
             stats = training and self.use_bn
             bb.y_recompute = training and not keep_y
             ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
-                            bb.part if stats else None)
+                            bb.part if stats else None, bb.zsel, gamma)
             if stats:
                 ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean,
                                 bb.rstd, bb.scale, bb.shift)
@@ -297,10 +301,14 @@ class UNetEngine:
         ops.dwconv3x3_fwd(view, n, h, w, dk, bb.y)
         if training and self.use_bn:
             ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, bb.part)
+        else:
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, None)
+        if bb.zsel is not None:
+            ops.pool_select(bb.z, n, h, w, b.cout, gamma, bb.zsel)
+        if training and self.use_bn:
             ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
                             bb.scale, bb.shift)
         else:
-            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, None)
             ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
         return View.bnrelu(bb.z, bb.scale, bb.shift)
 
@@ -370,7 +378,8 @@ class UNetEngine:
             v = self._block_fwd(A, b1, v, training)
             self._block_fwd(A, b2, v, training)
             bb = A.blocks[b2.name]
-            v = View.pool_bnrelu(bb.z, bb.scale, bb.shift)
+            # MaxPooling2D (model/u_net.py:69) read as a BN+ReLU view of the window selections
+            v = View.bnrelu(bb.zsel, bb.scale, bb.shift)
         v = self._block_fwd(A, self.bneck[0], v, training)
         v = self._block_fwd(A, self.bneck[1], v, training)
         if drop:
@@ -468,10 +477,13 @@ class UNetEngine:
         return tb.bnpart[:need]
 
     def _block_bwd(self, A: Acts, b: Block, view_in: View, dx0, dx1=None, drop_rate=0.0, drop_seed=0,
-                   stats_target: Optional[BlockBufs] = None):
+                   stats_target: Optional[BlockBufs] = None, view_f: Optional[View] = None):
         """Backward of one conv_block.  stats_target: the block whose output view_in reads (through
         BN+ReLU or the max-pool) when this launch completes its da (dx0); the depthwise data
-        gradient then also emits that block's BN-backward partials."""
+        gradient then also emits that block's BN-backward partials.  view_f: the same input as
+        view_in for the weight gradients when it reads cheaper (a max-pool input as the BN+ReLU
+        view of its window selections; the data gradient routes through the POOL view of z)."""
+        view_f = view_in if view_f is None else view_f
         n = A.n
         h, w = self._dims(b.level)
         m = n * h * w
@@ -513,11 +525,11 @@ class UNetEngine:
 
         def weight_grads():
             if bb.y_recompute:  # both kernels' gradients in one pass, y recomputed from view_in
-                ops.sepconv_bwd_filter(view_in, n, h, w, dk, dy, dz, b.cout, gdk, gpk)
+                ops.sepconv_bwd_filter(view_f, n, h, w, dk, dy, dz, b.cout, gdk, gpk)
                 return
             if not img_wg:  # (the image block's was accumulated by its data-gradient pass)
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            ops.dwconv3x3_bwd_filter(view_in, n, h, w, dy, gdk)
+            ops.dwconv3x3_bwd_filter(view_f, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 ops.copy_strided(gpk, 1, b.wcin * b.cout, b.cin * b.cout,
                                  self.gvars[f"{b.name}_sepconv/pointwise_kernel"], b.wcin * b.cout)
@@ -617,13 +629,15 @@ class UNetEngine:
                         drop_seed=seeds["bneck_dropout"] if drop else 0, stats_target=A.blocks[b1.name])
         e4 = A.blocks[self.enc[-1][2].name]
         # pooled half ACCUMULATES into the encoder block's da (the skip half is already there)
-        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, stats_target=e4)
+        self._block_bwd(A, b1, View.pool_bnrelu(e4.z, e4.scale, e4.shift), e4.da, stats_target=e4,
+                        view_f=View.bnrelu(e4.zsel, e4.scale, e4.shift))
         for j in reversed(range(len(self.enc))):
             stage, e1, e2 = self.enc[j]
             self._block_bwd(A, e2, self._view_of(A, e1), A.blocks[e1.name].da, stats_target=A.blocks[e1.name])
             if j > 0:
                 pb = A.blocks[self.enc[j - 1][2].name]
-                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb)
+                self._block_bwd(A, e1, View.pool_bnrelu(pb.z, pb.scale, pb.shift), pb.da, stats_target=pb,
+                                view_f=View.bnrelu(pb.zsel, pb.scale, pb.shift))
             else:
                 self._block_bwd(A, e1, View.plain(self._x_last), None)
         self._flush_side()

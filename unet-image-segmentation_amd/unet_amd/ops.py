@@ -343,8 +343,11 @@ def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
 
 
 def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tensor, y: Optional[Tensor],
-                z: Tensor, partials: Optional[Tensor] = None):
-    """Fused depthwise 3x3 + pointwise 1x1 (+ BN partials); y (depthwise output) optional."""
+                z: Tensor, partials: Optional[Tensor] = None, zsel: Optional[Tensor] = None,
+                gamma: Optional[Tensor] = None):
+    """Fused depthwise 3x3 + pointwise 1x1 (+ BN partials); y (depthwise output) optional; zsel
+    (optional, (n, h/2, w/2, cout)): the 2x2 max-pool selection of z for the next stage (see
+    unet_pool_select; gamma = the block's BN gamma, None without BatchNorm)."""
     C = x.channels
     m = n * h * w
     _check(dk, "depthwise_kernel", 9 * C)
@@ -354,10 +357,25 @@ def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tens
         _check(y, "y", m * C)
     if partials is not None:
         _check(partials, "bn_partials", bn_partials_numel(m, cout))
+    if zsel is not None:
+        _check(zsel, "z_pool_sel", m * cout // 4)
+    if gamma is not None:
+        _check(gamma, "gamma", cout)
     vs = x.c_struct()
-    _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C,
-                               x.src_bytes(n, h, w) + 4.0 * (m * cout + C * cout + 9 * C)),
-          ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _stream())
+    nb = x.src_bytes(n, h, w) + 4.0 * (m * cout + C * cout + 9 * C) + (4.0 * m * C if y is not None else 0.0) + \
+        (1.0 * m * cout if zsel is not None else 0.0)
+    _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C, nb),
+          ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _ptr(zsel),
+          _ptr(gamma), _stream())
+
+
+def pool_select(z: Tensor, n: int, h: int, w: int, c: int, gamma: Optional[Tensor], out: Tensor):
+    """out (n, h/2, w/2, c): per 2x2 window the raw z the max-pool of relu(bn(z)) selects."""
+    _check(z, "z", n * h * w * c)
+    _check(out, "out", n * h * w * c // 4)
+    if gamma is not None:
+        _check(gamma, "gamma", c)
+    _call("unet_pool_select", (0.0, 5.0 * n * h * w * c), _ptr(z), n, h, w, c, _ptr(gamma), _ptr(out), _stream())
 
 
 def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
