@@ -89,7 +89,7 @@ def op_breakdown(summary):
     return rows
 
 
-def encoder_block_roofline(batch, size, device, reps=10):
+def encoder_block_roofline(batch, size, device, reps=10, x3=True):
     """forward, training-mode conv blocks of the encoder (depthwise -> pointwise +
     BN-statistics epilogue; the BN apply + ReLU of the input is done on load, as in the train
     step) at `batch` images, each timed with HIP events around `reps` back-to-back launches (median
@@ -126,6 +126,10 @@ def encoder_block_roofline(batch, size, device, reps=10):
             # 64 x 64 level up, y stored unless the block's weight gradients recompute it; split
             # depthwise + pointwise launches (y always stored) below
             fused, keep_y = block_fwd_choice(view, batch, hh, hh, co, training=True)
+            pkx = None  # the split-precision weight planes the engine hands the fused kernel
+            if fused and x3 and ck % 16 == 0 and ck >= 64:
+                pkx = torch.empty(3 * ck * co, dtype=torch.int16, device=device)
+                ops.split_x3(pk, [(0, ck, co, 0)], pkx)
             ybuf = torch.empty((batch, hh, hh, ck), device=device)
             z = torch.empty((batch, hh, hh, co), device=device)
             part = torch.zeros(ops.bn_partials_numel(m, co), device=device)
@@ -135,7 +139,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
 
             def run():
                 if fused:
-                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf if keep_y else None, z, part, zsel, gam)
+                    ops.sepconv_fwd(view, batch, hh, hh, dk, co, pk, ybuf if keep_y else None, z, part, zsel, gam,
+                                    pkx)
                 else:
                     ops.dwconv3x3_fwd(view, batch, hh, hh, dk, ybuf)
                     ops.pointwise_fwd(ybuf, m, ck, co, pk, z, part)
@@ -157,7 +162,8 @@ def encoder_block_roofline(batch, size, device, reps=10):
             nb = 4.0 * (m * (ci + co) + 9 * ci + ci * co + 4 * co)
             t_roof = max(fl / (PEAK_FP32_TFLOPS * 1e12), nb / (PEAK_HBM_GBS * 1e9)) * 1e6
             rows.append({"block": f"enc{lvl + 1}_block{blk + 1}", "hw": hh, "cin": ci, "cout": co,
-                         "kernel": ("unet_sepconv_fwd" + (" (+y store)" if keep_y else "") if fused
+                         "kernel": ("unet_sepconv_fwd" + (" bf16x6" if pkx is not None else "") +
+                                    (" (+y store)" if keep_y else "") if fused
                                     else "dwconv3x3_fwd+pointwise_fwd") + (" +pool select" if blk == 1 else "") +
                                    (f" (input padded {ci}->{ck} ch)" if ck != ci else ""),
                          "bound": "mfma" if fl / nb >= RIDGE else "hbm", "us": round(us, 1),
@@ -269,6 +275,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline timed steps (median reported)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: physical cores, capped)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-x3", action="store_true",
+                    help="fp32-MFMA fused forward instead of its split-precision (bf16x6) variant (A/B)")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -299,6 +307,7 @@ def main():
                   metrics=[MeanIoU(num_classes=2, name="mean_io_u", device=device), "dice_coef"])
     if world > 1:
         model.enable_data_parallel()
+    model.engine.use_x3 = not args.no_x3
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
 
     for _ in range(args.warmup):
@@ -388,7 +397,7 @@ def main():
         if not args.no_roofline and world == 1 and args.encoder_batch > 0:
             del model
             torch.cuda.empty_cache()
-            out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device)
+            out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device, x3=not args.no_x3)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes, args.batch, args.cpu_warmup,
                                                args.cpu_steps, args.cpu_threads)

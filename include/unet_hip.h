@@ -86,6 +86,15 @@ int unet_stream_wait_stream(unet_stream_t waiter, unet_stream_t producer,
 int unet_copy_strided(const float* src, int64_t rows, int cols, int64_t src_ld, float* dst,
                       int64_t dst_ld, unet_stream_t stream);
 
+/* Split-precision weights: for each segment i (segs[4 i .. 4 i + 3] = source offset, rows,
+ * cols, destination offset; host array, offsets in elements), dst + dst_off holds three bf16
+ * planes [3][cols][rows] (transposed) with src[r][c] == hi + mid + lo exactly (round-to-nearest
+ * bf16 of the value, then of each remainder).  One launch for every pointwise kernel of a step.
+ * dst offsets must be multiples of 8 (16-B planes); rows * cols per plane.                  */
+#define UNET_SPLIT_MAX_SEGS 32
+int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                  unet_stream_t stream);
+
 /* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
  * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers
  * read views directly); it serves eager conv_block outputs and inspection.                 */
@@ -155,9 +164,16 @@ int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
  * unet_sepconv_fwd_supported() says so (h % 8 == 0, w % 16 == 0, channels % 4 == 0).     */
 int unet_sepconv_fwd_supported(const unet_view* x, int n, int h, int w, int cout);
 int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                     int cout, const float* pw_kernel, float* y, float* z,
+                     int cout, const float* pw_kernel,
+                     const unsigned short* pw_kernel_x3, float* y, float* z,
                      float* bn_partials, float* z_pool_sel, const float* gamma,
                      unet_stream_t stream);
+/* pw_kernel_x3 (optional): pw_kernel split by unet_split_x3 ([3][Cout][Cin] bf16 planes).  With
+ * it the register-A kernel runs its split-precision MFMA variant where it exists (channels
+ * % 16 == 0, no max-pool view): every product of the pointwise GEMM is formed from the three
+ * bf16 parts of both operands, x == hi + mid + lo exactly, and summed as the six significant
+ * part products on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (error ~2^-23 |a b| per
+ * product, below fp32 accumulation rounding: DESIGN.md "Split-precision MFMA").              */
 /* z_pool_sel (optional, (N, h/2, w/2, cout)): the encoder stage's MaxPooling2D((2,2))
  * (model/u_net.py:69) prepared for its consumer: per 2x2 window of z and channel, the raw
  * value the max-pool of relu(z * scale + shift) selects -- the window max where gamma >= 0,

@@ -788,3 +788,39 @@ def test_sepconv_pool_selection_epilogue(ops, sep_schedule, mode, n, h, w, c0, c
     ref = torch.empty_like(zsel)
     ops.pool_select(z, n, h, w, cout, gamma, ref)
     assert torch.equal(zsel, ref)
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", [(1, 2, 8, 16, 64, 0, 64, 0.0), (1, 1, 16, 32, 128, 0, 128, 0.0),
+                                                        (3, 1, 16, 16, 64, 64, 64, 0.2), (0, 2, 8, 32, 96, 0, 192, 0.0),
+                                                        (1, 1, 8, 16, 256, 0, 256, 0.0)])
+def test_fused_sepconv_split_precision(ops, mode, n, h, w, c0, c1, cout, drop):
+    """The register-A kernel's bf16x6 variant (pw_kernel_x3 from unet_split_x3): z within the fp32
+    path's tolerance of the float64 oracle, the depthwise output y bitwise equal to the fp32
+    variant's (same taps, same fmaf order), BN partials consistent."""
+    rng = np.random.default_rng(300 + mode + cout)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = dev(f32(rng.standard_normal((3, 3, C, 1))))
+    pk32 = f32(rng.standard_normal((1, 1, C, cout)) / np.sqrt(C))
+    pk = dev(pk32)
+    pkx = torch.empty(3 * C * cout, dtype=torch.int16, device="cuda")
+    ops.split_x3(pk, [(0, C, cout, 0)], pkx)
+    # the planes hold the exact three-way split, transposed
+    hm = pkx.view(3, cout, C).cpu().numpy().astype(np.uint16).astype(np.uint32) << 16
+    parts = hm.view(np.float32).astype(np.float64)
+    assert np.array_equal(parts.sum(0), pk32[0, 0].astype(np.float64).T)
+    v = _mk_view(ops, mode, t, drop, 77)
+    m = n * h * w
+    outs = {}
+    for tag, px in (("f32", None), ("x6", pkx)):
+        y = torch.full((n, h, w, C), -7.0, device="cuda")
+        z = torch.empty((n, h, w, cout), device="cuda")
+        part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
+        ops.sepconv_fwd(v, n, h, w, dk, cout, pk, y, z, part, pkx=px)
+        outs[tag] = (y, z, part)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 77)
+    zr = K.pointwise(K.depthwise3x3(xv, host(dk)), pk32)
+    assert rel_err(host(outs["x6"][1]), zr) < 5e-6
+    assert rel_err(host(outs["x6"][1]), zr) <= 2 * rel_err(host(outs["f32"][1]), zr) + 1e-7
+    assert torch.equal(outs["x6"][0], outs["f32"][0])
+    assert rel_err(host(outs["x6"][2]), host(outs["f32"][2])) < 1e-5

@@ -1231,19 +1231,22 @@ void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
     else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
 }
 
-// Split-precision (bf16x6) rows GEMM: 128 x 128 tiles, BK 16 or 32 (lab A/B: UNET_X6)
+// Split-precision (bf16x6) rows / wgrad GEMMs: lab build only (UNET_X6).  Measured (tools/bench_rows.py,
+// profiles/r3_x6_rows_ab.jsonl): no faster than fp32 MFMA here -- these GEMMs are load-latency
+// bound (MFMA pipe 27-54 % busy, PMC profiles/r3c_pmc_rows*.csv), so fewer MFMA cycles do not show.
 bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
 
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     if (rows_vec_ok(a, AMODE)) {
         const RowsCfg c = rows_cfg(a, AMODE);
+#ifdef UNET_LAB_BUILD  // (not compiled into the product library)
         if (rows_x6()) {
-            if (c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI, true>(a, st);
-            else launch_rows_tile<128, 16, AMODE, DROP, EPI, true>(a, st);
+            launch_rows_tile<128, 16, AMODE, DROP, EPI, true>(a, st);
             UNET_CHECK_LAUNCH(what);
             return 0;
         }
+#endif
         if (c.bn == 64 && c.bk == 16) launch_rows_tile<64, 16, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 64 && c.bk == 32) launch_rows_tile<64, 32, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 128 && c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI>(a, st);
@@ -1298,9 +1301,13 @@ void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
                      (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
                      ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
     if (vec || BMODE == W_BNBWD) {
-        if (w.bp == 128 && w.bq == 128 && wgrad_x6())
+#ifdef UNET_LAB_BUILD
+        if (w.bp == 128 && w.bq == 128 && wgrad_x6()) {
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP, true><<<grid, 256, 0, st>>>(a);
-        else if (w.bp == 128 && w.bq == 128)
+            return;
+        }
+#endif
+        if (w.bp == 128 && w.bq == 128)
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
         else if (w.bp == 128)
             gemm_wgrad_vec<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);

@@ -287,6 +287,75 @@ extern "C" int unet_copy_strided(const float* src, int64_t rows, int cols, int64
     return 0;
 }
 
+namespace unet {
+namespace {
+struct SplitTable {
+    int n;
+    int64_t src[UNET_SPLIT_MAX_SEGS], dst[UNET_SPLIT_MAX_SEGS];
+    int rows[UNET_SPLIT_MAX_SEGS], cols[UNET_SPLIT_MAX_SEGS];
+};
+// dst planes [3][cols][rows] (bf16 bits) of src [rows][cols]: a 32 x 32 tile per block through LDS,
+// read along cols and written along rows (blockIdx.y = segment)
+__global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ src, SplitTable t,
+                                                       unsigned short* __restrict__ dst) {
+    __shared__ float T[32][33];
+    const int s = blockIdx.y;
+    const int rows = t.rows[s], cols = t.cols[s];
+    const int tr = (rows + 31) / 32, tc = (cols + 31) / 32;
+    const float* S = src + t.src[s];
+    unsigned short* D = dst + t.dst[s];
+    const int64_t plane = (int64_t)rows * cols;
+    for (int tile = blockIdx.x; tile < tr * tc; tile += gridDim.x) {
+        const int r0 = (tile / tc) * 32, c0 = (tile % tc) * 32;
+        __syncthreads();
+        for (int i = threadIdx.x; i < 1024; i += 256) {
+            const int r = r0 + (i >> 5), c = c0 + (i & 31);
+            T[i >> 5][i & 31] = (r < rows && c < cols) ? S[(int64_t)r * cols + c] : 0.f;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 1024; i += 256) {
+            const int c = c0 + (i >> 5), r = r0 + (i & 31);
+            if (r < rows && c < cols) {
+                const float x = T[i & 31][i >> 5];
+                const unsigned h = bf16_bits(x);
+                const float rr = x - bf16_val(h);
+                const unsigned m = bf16_bits(rr);
+                const unsigned l = bf16_bits(rr - bf16_val(m));
+                const int64_t o = (int64_t)c * rows + r;
+                D[o] = (unsigned short)h;
+                D[plane + o] = (unsigned short)m;
+                D[2 * plane + o] = (unsigned short)l;
+            }
+        }
+    }
+}
+}  // namespace
+}  // namespace unet
+
+extern "C" int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                             unet_stream_t stream) {
+    UNET_CHECK_ARG(src && segs && dst && nseg > 0 && nseg <= UNET_SPLIT_MAX_SEGS, "unet_split_x3: bad arguments");
+    unet::SplitTable t{};
+    t.n = nseg;
+    int maxtiles = 1;
+    for (int i = 0; i < nseg; ++i) {
+        const int64_t so = segs[4 * i], rows = segs[4 * i + 1], cols = segs[4 * i + 2], doff = segs[4 * i + 3];
+        UNET_CHECK_ARG(so >= 0 && doff >= 0 && rows > 0 && cols > 0 && rows < (1 << 30) && cols < (1 << 30),
+                       "unet_split_x3: bad segment %d", i);
+        UNET_CHECK_ARG(doff % 8 == 0, "unet_split_x3: segment %d destination must be 16-B aligned", i);
+        t.src[i] = so;
+        t.dst[i] = doff;
+        t.rows[i] = (int)rows;
+        t.cols[i] = (int)cols;
+        const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
+        if (tiles > maxtiles) maxtiles = tiles > 1024 ? 1024 : (int)tiles;
+    }
+    unet::split_x3_kernel<<<dim3((unsigned)maxtiles, (unsigned)nseg), 256, 0, static_cast<hipStream_t>(stream)>>>(
+        src, t, dst);
+    UNET_CHECK_LAUNCH("unet_split_x3");
+    return 0;
+}
+
 extern "C" int unet_abi_version(void) { return UNET_ABI_VERSION; }
 extern "C" const char* unet_last_error(void) { return unet::g_err; }
 

@@ -21,6 +21,7 @@ struct SepArgs {
     float* y;         // optional (N,H,W,Cin)
     float* z;         // (N,H,W,Cout)
     float2* stats;    // [M/128][Cout]
+    const unsigned short* pkx;  // optional bf16x3 split of pk: planes [3][Cout][Cin] (unet_split_x3)
     float* zsel;         // optional (N,H/2,W/2,Cout): the 2x2 pooling selection of z (pool_select_kernel)
     const float* gamma;  // zsel: BN gamma (its sign orders the window), NULL = no BN (max)
 };
@@ -32,8 +33,10 @@ __device__ __forceinline__ float pool_sel(float a, float b, float c, float d, bo
     return neg ? fminf(fminf(a, b), fminf(c, d)) : fmaxf(fmaxf(a, b), fmaxf(c, d));
 }
 
-// register-A schedule (sepconv_rk.hip): returns 0, or -1 if the mode/shape has no such kernel
+// register-A schedule (sepconv_rk.hip): returns 0, or -1 if the mode/shape has no such kernel.
+// With a.pkx (and Cin % 16 == 0, no max-pool view) the split-precision (bf16x6) variant runs.
 int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);
+bool rk_x6_supported(int mode, int cin);
 bool rk_supported(int mode, int cin, int cout);
 
 }  // namespace sep

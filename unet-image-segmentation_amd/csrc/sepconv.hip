@@ -433,8 +433,8 @@ extern "C" int unet_pool_select(const float* z, int n, int h, int w, int c, cons
 }
 
 extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const float* dw_kernel, int cout,
-                                const float* pw_kernel, float* y, float* z, float* bn_partials, float* z_pool_sel,
-                                const float* gamma, unet_stream_t stream) {
+                                const float* pw_kernel, const unsigned short* pw_kernel_x3, float* y, float* z,
+                                float* bn_partials, float* z_pool_sel, const float* gamma, unet_stream_t stream) {
     if (check_view(x, "unet_sepconv_fwd")) return -1;
     UNET_CHECK_ARG(unet_sepconv_fwd_supported(x, n, h, w, cout),
                    "unet_sepconv_fwd: unsupported shape (needs h%%8==0, w%%16==0, channels%%4==0)");
@@ -459,12 +459,14 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     }
     if (z_pool_sel && !(g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout))) {
         // LDS-A-tile schedule: the selection in a pass over z after the kernel
-        const int rc = unet_sepconv_fwd(x, n, h, w, dw_kernel, cout, pw_kernel, y, z, bn_partials, nullptr, nullptr,
-                                        stream);
+        const int rc = unet_sepconv_fwd(x, n, h, w, dw_kernel, cout, pw_kernel, pw_kernel_x3, y, z, bn_partials,
+                                        nullptr, nullptr, stream);
         return rc ? rc : unet_pool_select(z, n, h, w, cout, gamma, z_pool_sel, stream);
     }
     a.zsel = z_pool_sel;
     a.gamma = gamma;
+    UNET_CHECK_ARG(((uintptr_t)pw_kernel_x3 & 15) == 0, "unet_sepconv_fwd: pw_kernel_x3 must be 16-B aligned");
+    a.pkx = pw_kernel_x3;
     // register-A schedule where it exists (BN+ReLU / concat / plain views, >= 64 channels) unless
     // the LDS-A-tile schedule is forced; max-pool views keep the LDS-A-tile kernel (4 raw loads
     // per halo element need its wider 8-wave staging)

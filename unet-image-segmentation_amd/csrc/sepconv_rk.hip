@@ -34,24 +34,34 @@ constexpr int HPIX = HHp * HWp;            // 180 halo pixels
 
 // tile column of the pixel that lane lo (0..31) of a wave owns (row 2w + (lo >> 4))
 __device__ __forceinline__ int rk_col(int lo) { return lo < 16 ? lo : ((lo + 14) & 15); }
-template <int BN>
+template <int BN, bool X6 = false>
 struct RkLds {
-    static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = BK * (BN + 4);
+    // X6: B as three bf16 planes [BN][16 k] (32-byte rows; the two 16-byte k chunks of row n are
+    // swapped when bit 3 of n is set, so the fragment reads of 16-lane groups are conflict-free)
+    static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = X6 ? 3 * BN * BK / 2 : BK * (BN + 4);
     static constexpr int RING = 3 * (XSZ + KSZ + BSZ);
     static constexpr int TLD = BN + 4;                 // epilogue transpose row stride
     static constexpr int EPI = 4 * 32 * TLD + 4 * BN;  // 4 waves' tiles + the statistics combine
     static constexpr int SIZE = RING > EPI ? RING : EPI;
 };
 
-template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y>
+// X6 (split precision; no max-pool views, Cin % 16 == 0): per 16-channel stage each lane evaluates
+// the depthwise output of its pixel for the 8 channels 8 (l >> 5) + j of v_mfma_f32_32x32x16_bf16's
+// A operand (same taps, same fmaf order: y bitwise equal), splits them into three bf16 fragments
+// (common.h split4) and runs mfma_x6 against the pre-split weight planes (SepArgs::pkx) per 32-column
+// tile: 6 x 32 MFMA cycles per stage and tile instead of 8 x 64.
+template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y, bool X6 = false>
 __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
+    static_assert(!X6 || MODE != UNET_VIEW_POOL_BNRELU, "X6: no max-pool views");
     constexpr int TN = BN / 32;                 // MFMA tiles per wave (all BN columns)
     constexpr int NH = HPIX * (BK / 4);         // halo float4 per stage (720)
     constexpr int HR = (NH + 255) / 256;        // per thread (3)
     constexpr int NP = MODE == UNET_VIEW_POOL_BNRELU ? 4 : 1;
-    constexpr int BQ = BN * (BK / 4) / 256;     // B float4 per thread per stage
+    constexpr int BQ = X6 ? 1 : BN * (BK / 4) / 256;  // B float4 per thread per stage
     constexpr int LB = BN + 4;                  // k-major B row stride
-    using L = RkLds<BN>;
+    constexpr int BXN = 3 * BN * 2;             // X6: 16-byte B chunks per stage
+    constexpr int BXC = X6 ? (BXN + 255) / 256 : 1;
+    using L = RkLds<BN, X6>;
     __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     auto Xs = [&](int b) { return smem + b * L::XSZ; };
     auto Ks = [&](int b) { return smem + 3 * L::XSZ + b * L::KSZ; };
@@ -173,6 +183,28 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
         for (int r = 0; r < BQ; ++r)
             *reinterpret_cast<float4*>(&Bs(buf)[(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
     };
+    // X6 B staging: 16-byte chunks (plane, column, k half) of the pre-split planes, clamped loads
+    uint4 rbx[BXC];
+    bool bxok[BXC];
+    auto load_bx = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < BXC; ++j) {
+            const int e = tid + 256 * j, pl = e / (2 * BN), r = e - pl * 2 * BN, nn = r >> 1, c = r & 1;
+            bxok[j] = e < BXN && n0 + nn < g.Cout && k0 + 8 * c < Cin;
+            rbx[j] = *reinterpret_cast<const uint4*>(
+                g.pkx + (bxok[j] ? ((int64_t)pl * g.Cout + n0 + nn) * Cin + k0 + 8 * c : 0));
+        }
+    };
+    auto store_bx = [&](int buf) {
+        unsigned short* Bb = reinterpret_cast<unsigned short*>(Bs(buf));
+#pragma unroll
+        for (int j = 0; j < BXC; ++j) {
+            const int e = tid + 256 * j, pl = e / (2 * BN), r = e - pl * 2 * BN, nn = r >> 1, c = r & 1;
+            if (e < BXN)
+                *reinterpret_cast<uint4*>(Bb + (pl * BN + nn) * BK + 8 * (c ^ ((nn >> 3) & 1))) =
+                    bxok[j] ? rbx[j] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
 
     // ---- this lane's pixel: tile row 2 wave + (lo >> 4), column rk_col(lo)
     const int pr = 2 * wave + (lo >> 4), pc = rk_col(lo);
@@ -236,6 +268,76 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     // while the global loads of stage kt+2 are in flight; they are written into slot (kt+2) % 3,
     // last read during stage kt-1.  One barrier per stage.
     const int nk = (Cin + BK - 1) / BK;
+    if constexpr (X6) {
+        // depthwise of this lane's pixel, channels 8 hi + 0..7 of the stage, from halo / taps b
+        const int xoff8 = (pr * HWp + pc) * RX + 8 * hi;
+        auto dw8 = [&](int b, float4& o0, float4& o1) {
+            const float* X = Xs(b);
+            const float* Kt = Ks(b);
+            o0 = f4(0.f);
+            o1 = f4(0.f);
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const float* xp = &X[xoff8 + (dy * HWp + dx) * RX];
+                    const float* kp = &Kt[(dy * 3 + dx) * BK + 8 * hi];
+                    o0 = fma4(*reinterpret_cast<const float4*>(xp), *reinterpret_cast<const float4*>(kp), o0);
+                    o1 = fma4(*reinterpret_cast<const float4*>(xp + 4), *reinterpret_cast<const float4*>(kp + 4), o1);
+                }
+        };
+        float* yrow8 = nullptr;
+        if constexpr (WRITE_Y) yrow8 = g.y + ((int64_t)(n * g.H + h0 + pr) * g.W + w0 + pc) * Cin + 8 * hi;
+        load_halo(0);
+        load_bx(0);
+        store_halo(0);
+        store_bx(0);
+        load_halo(BK);
+        load_bx(BK);
+        store_halo(1);
+        store_bx(1);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cb = kt % 3, wb = (kt + 2) % 3;
+            load_halo((kt + 2) * BK);
+            load_bx((kt + 2) * BK);
+            // this stage's depthwise (VALU), then its MFMAs: with two waves per SIMD one wave's
+            // depthwise runs beside the other's MFMAs (a look-ahead inside the wave needed ~60 more
+            // registers and spilled)
+            float4 a0, a1;
+            dw8(cb, a0, a1);
+            if constexpr (WRITE_Y) {
+                const int k0 = kt * BK;
+                if (blockIdx.y == 0 && k0 < Cin) {
+                    st4(yrow8 + k0, a0);
+                    st4(yrow8 + k0 + 4, a1);
+                }
+            }
+            bf16x8 af[3];
+            {
+                const Split4 s0 = split4(a0), s1 = split4(a1);
+                af[0] = __builtin_bit_cast(bf16x8, make_uint4(s0.h.x, s0.h.y, s1.h.x, s1.h.y));
+                af[1] = __builtin_bit_cast(bf16x8, make_uint4(s0.m.x, s0.m.y, s1.m.x, s1.m.y));
+                af[2] = __builtin_bit_cast(bf16x8, make_uint4(s0.l.x, s0.l.y, s1.l.x, s1.l.y));
+            }
+            const unsigned short* Bb = reinterpret_cast<const unsigned short*>(Bs(cb));
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int nn = tn * 32 + lo;
+                const int cs = hi ^ ((nn >> 3) & 1);
+                bf16x8 bfr[3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    bfr[pl] = *reinterpret_cast<const bf16x8*>(Bb + (pl * BN + nn) * BK + 8 * cs);
+                acc[tn] = mfma_x6(af, bfr, acc[tn]);
+            }
+            if (kt + 2 < nk) {
+                store_halo(wb);
+                store_bx(wb);
+            }
+            __syncthreads();
+        }
+    } else {
     load_halo(0);
     load_b(0);
     store_halo(0);
@@ -268,6 +370,7 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
             store_b(wb);
         }
         __syncthreads();
+    }
     }
 
     // ---- epilogue (the loop ended on a barrier: the ring is free).  Accumulator row
@@ -360,19 +463,32 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     }
 }
 
-template <int MODE, bool DROP, int BN>
-void launch_rk_t(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
+template <int MODE, bool DROP, int BN, bool X6>
+void launch_rk_x(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
     const dim3 grid((unsigned)(a.N * (a.H / TH) * (a.W / TW)), (unsigned)cdiv(a.Cout, BN));
     if (stats) {
-        if (write_y) sepconv_rk_kernel<MODE, DROP, E_STATS, BN, true><<<grid, 256, 0, st>>>(a);
-        else sepconv_rk_kernel<MODE, DROP, E_STATS, BN, false><<<grid, 256, 0, st>>>(a);
+        if (write_y) sepconv_rk_kernel<MODE, DROP, E_STATS, BN, true, X6><<<grid, 256, 0, st>>>(a);
+        else sepconv_rk_kernel<MODE, DROP, E_STATS, BN, false, X6><<<grid, 256, 0, st>>>(a);
     } else {
-        if (write_y) sepconv_rk_kernel<MODE, DROP, E_STORE, BN, true><<<grid, 256, 0, st>>>(a);
-        else sepconv_rk_kernel<MODE, DROP, E_STORE, BN, false><<<grid, 256, 0, st>>>(a);
+        if (write_y) sepconv_rk_kernel<MODE, DROP, E_STORE, BN, true, X6><<<grid, 256, 0, st>>>(a);
+        else sepconv_rk_kernel<MODE, DROP, E_STORE, BN, false, X6><<<grid, 256, 0, st>>>(a);
     }
 }
 
+template <int MODE, bool DROP, int BN>
+void launch_rk_t(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
+    if constexpr (MODE != UNET_VIEW_POOL_BNRELU) {
+        if (a.pkx && rk_x6_supported(MODE, a.Cin)) {
+            launch_rk_x<MODE, DROP, BN, true>(a, stats, write_y, st);
+            return;
+        }
+    }
+    launch_rk_x<MODE, DROP, BN, false>(a, stats, write_y, st);
+}
+
 }  // namespace
+
+bool rk_x6_supported(int mode, int cin) { return mode != UNET_VIEW_POOL_BNRELU && cin % 16 == 0 && cin >= 64; }
 
 bool rk_supported(int mode, int cin, int cout) {
     // max-pool views only up to 128 output channels: wider layers keep the LDS-A-tile kernel's

@@ -61,7 +61,8 @@ SIGNATURES = {
     "unet_pointwise_bwd_filter_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_filter": (c_int, [P, P, c_int64, c_int, c_int, P, P, c_size_t, P]),
     "unet_sepconv_fwd_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
-    "unet_sepconv_fwd": (c_int, [_VP, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P]),
+    "unet_sepconv_fwd": (c_int, [_VP, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P]),
+    "unet_split_x3": (c_int, [P, P, c_int, P, P]),
     "unet_pool_select": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),

@@ -76,7 +76,7 @@ class PairLoader:
     are deterministic, so the batches are identical to decoding every epoch."""
 
     def __init__(self, frames_dir, masks_dir, size, batch_size, seed, shuffle=True, horizontal_flip=False, rank=0,
-                 world=1, workers=8, cache_bytes=16 << 30):
+                 world=1, workers=16, cache_bytes=16 << 30):
         if batch_size < world:
             raise ValueError(f"batch size {batch_size} < {world} data-parallel ranks: every rank needs a sample")
         self.frames = [os.path.join(frames_dir, f) for f in _list(frames_dir)]

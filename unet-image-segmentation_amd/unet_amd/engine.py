@@ -144,8 +144,10 @@ class UNetEngine:
             else:
                 o = self.stat_layout.offsets[s.name]
                 self.vars[s.name] = self.stats[o:o + s.size].view(s.shape)
+        self.params_version = 0  # bumped whenever the trainable weights change (split planes go stale)
         self.set_weights_dict(init_weights(self.specs, self.seed))
         self._build_plan()
+        self._build_x3()
         self._acts: Dict[int, Acts] = {}
         self.step_count = 0
         self.rank_salt = 0  # data-parallel rank (dropout streams); set by model.enable_data_parallel
@@ -193,6 +195,35 @@ class UNetEngine:
             if tuple(a.shape) != tuple(t.shape):
                 raise ValueError(f"{name}: shape {a.shape} != {tuple(t.shape)}")
             t.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(self.device))
+
+        self.params_version += 1
+
+    def _build_x3(self):
+        """Split-precision planes (ops.split_x3) of the pointwise kernels of the blocks whose fused
+        forward can run the bf16x6 register-A kernel (>= 64 x 64 pixels, channels % 16 == 0):
+        one launch per weight update refreshes all of them."""
+        self.use_x3 = True
+        self.x3_off: Dict[str, int] = {}
+        segs, off = [], 0
+        for b in self.blocks:
+            h, w = self._dims(b.level)
+            if h * w >= FUSE_MIN_PIXELS and b.cin % 16 == 0 and b.cin >= 64 and not b.wcin:
+                src = self.train_layout.offsets[f"{b.name}_sepconv/pointwise_kernel"]
+                segs.append((src, b.cin, b.cout, off))
+                self.x3_off[b.name] = off
+                off += (3 * b.cin * b.cout + 7) // 8 * 8
+        self.x3_segs = segs
+        self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
+        self._x3_version = -1
+
+    def _refresh_x3(self):
+        if self.use_x3 and self.x3_segs and self._x3_version != self.params_version:
+            ops.split_x3(self.params, self.x3_segs, self.pkx)
+            self._x3_version = self.params_version
+
+    def _pkx(self, b: "Block"):
+        o = self.x3_off.get(b.name) if self.use_x3 else None
+        return None if o is None else self.pkx[o:o + 3 * b.cin * b.cout]
 
     def get_weights_dict(self) -> Dict[str, np.ndarray]:
         return {s.name: self.vars[s.name].detach().cpu().numpy().copy() for s in self.specs}
@@ -290,7 +321,7 @@ class UNetEngine:
             stats = training and self.use_bn
             bb.y_recompute = training and not keep_y
             ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
-                            bb.part if stats else None, bb.zsel, gamma)
+                            bb.part if stats else None, bb.zsel, gamma, self._pkx(b))
             if stats:
                 ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean,
                                 bb.rstd, bb.scale, bb.shift)
@@ -372,6 +403,7 @@ class UNetEngine:
         if drop and seeds is None:
             seeds = self.drop_seeds(self.step_count + 1)
         x = self._padded_input(A, x)
+        self._refresh_x3()
         self._x_fwd = x
         v = View.plain(x)
         for stage, b1, b2 in self.enc:

@@ -110,6 +110,7 @@ class UNetModel:
             self.engine.backward(y, self.loss_kind, loss_scale)
             scale = self.bucketer.finish() if self.bucketer is not None else 1.0
             self.optimizer.apply(self.engine.params, self.engine.grads, scale)
+            self.engine.params_version += 1
         caller.wait_stream(main)
         return res
 

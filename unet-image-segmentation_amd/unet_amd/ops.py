@@ -342,12 +342,28 @@ def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
     return bool(L.load().unet_sepconv_fwd_supported(ctypes.byref(vs), n, h, w, cout))
 
 
+def split_x3(src: Tensor, segs, dst: Tensor):
+    """bf16 x 3 split-precision planes of several weight matrices in one launch: segs = [(source
+    offset, rows, cols, destination offset)] in elements of src (float32) / dst (int16 holding
+    bf16 bits); each segment becomes planes [3][cols][rows] at its destination offset."""
+    if src.dtype != torch.float32 or dst.dtype != torch.int16:
+        raise TypeError("split_x3: float32 source, int16 (bf16 bits) destination")
+    flat = [int(v) for seg in segs for v in seg]
+    for so, r, c, do in segs:
+        if so + r * c > src.numel() or do + 3 * r * c > dst.numel():
+            raise ValueError("split_x3: segment out of range")
+    arr = (ctypes.c_int64 * len(flat))(*flat)
+    _call("unet_split_x3", (0.0, sum(10.0 * r * c for _, r, c, _ in segs)), _ptr(src), arr, len(segs), _ptr(dst),
+          _stream())
+
+
 def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tensor, y: Optional[Tensor],
                 z: Tensor, partials: Optional[Tensor] = None, zsel: Optional[Tensor] = None,
-                gamma: Optional[Tensor] = None):
+                gamma: Optional[Tensor] = None, pkx: Optional[Tensor] = None):
     """Fused depthwise 3x3 + pointwise 1x1 (+ BN partials); y (depthwise output) optional; zsel
     (optional, (n, h/2, w/2, cout)): the 2x2 max-pool selection of z for the next stage (see
-    unet_pool_select; gamma = the block's BN gamma, None without BatchNorm)."""
+    unet_pool_select; gamma = the block's BN gamma, None without BatchNorm); pkx (optional): pk's
+    split-precision planes from split_x3 (the kernel's bf16x6 MFMA variant where it exists)."""
     C = x.channels
     m = n * h * w
     _check(dk, "depthwise_kernel", 9 * C)
@@ -361,12 +377,14 @@ def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tens
         _check(zsel, "z_pool_sel", m * cout // 4)
     if gamma is not None:
         _check(gamma, "gamma", cout)
+    if pkx is not None and (pkx.dtype != torch.int16 or pkx.numel() < 3 * C * cout or not pkx.is_cuda):
+        raise ValueError("sepconv_fwd: pkx must be the int16 split planes of pk (3 * Cin * Cout)")
     vs = x.c_struct()
     nb = x.src_bytes(n, h, w) + 4.0 * (m * cout + C * cout + 9 * C) + (4.0 * m * C if y is not None else 0.0) + \
         (1.0 * m * cout if zsel is not None else 0.0)
     _call("unet_sepconv_fwd", (2.0 * m * C * cout + 18.0 * m * C, nb),
-          ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(y), _ptr(z), _ptr(partials), _ptr(zsel),
-          _ptr(gamma), _stream())
+          ctypes.byref(vs), n, h, w, _ptr(dk), cout, _ptr(pk), _ptr(pkx), _ptr(y), _ptr(z), _ptr(partials),
+          _ptr(zsel), _ptr(gamma), _stream())
 
 
 def pool_select(z: Tensor, n: int, h: int, w: int, c: int, gamma: Optional[Tensor], out: Tensor):
