@@ -277,6 +277,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-x3", action="store_true",
                     help="fp32-MFMA fused forward instead of its split-precision (bf16x6) variant (A/B)")
+    ap.add_argument("--no-fused-bwd", action="store_true",
+                    help="64-output blocks: data-gradient GEMM + side-stream weight-gradient pass instead of "
+                         "the fused block backward (A/B)")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -308,6 +311,7 @@ def main():
     if world > 1:
         model.enable_data_parallel()
     model.engine.use_x3 = not args.no_x3
+    model.engine.fuse_block_bwd = not args.no_fused_bwd
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
 
     for _ in range(args.warmup):

@@ -207,6 +207,18 @@ size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout)
 int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                             const float* dy, const float* dz, int cout, float* d_dw_kernel,
                             float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream);
+/* The same pass for a 64-output block ALSO doing the block's BatchNorm + ReLU backward and
+ * pointwise data gradient (model/u_net.py:14-25, the GradientTape of scripts/train.py:308): per
+ * pixel tile dz = scale (g - p - (z - mu) q), g = da [z scale + shift > 0] with coef = (mu, p, q)
+ * from unet_bn_relu_bwd_stats(_finish) (exactly unet_pointwise_bwd_data_bnrelu's dz), then
+ * dy = dz . pw_kernel^T (written out, for the depthwise data gradient), d_pw_kernel = y^T dz and
+ * d_dw_kernel as above; dz never goes to memory (bytes: da, z, the input view, dy).  No dropout
+ * on either side.  Workspace as unet_sepconv_bwd_filter.                                      */
+int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                           const float* pw_kernel, const float* da, const float* z,
+                           const float* scale, const float* shift, const float* coef, int cout,
+                           float* dy, float* d_dw_kernel, float* d_pw_kernel, void* ws,
+                           size_t ws_bytes, unet_stream_t stream);
 
 /* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
  * momentum 0.99, epsilon 1e-3, biased batch variance for both the output

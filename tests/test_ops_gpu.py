@@ -824,3 +824,56 @@ def test_fused_sepconv_split_precision(ops, mode, n, h, w, c0, c1, cout, drop):
     assert rel_err(host(outs["x6"][1]), zr) <= 2 * rel_err(host(outs["f32"][1]), zr) + 1e-7
     assert torch.equal(outs["x6"][0], outs["f32"][0])
     assert rel_err(host(outs["x6"][2]), host(outs["f32"][2])) < 1e-5
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1", [(1, 2, 8, 16, 64, 0), (1, 1, 16, 32, 64, 0), (3, 1, 8, 32, 64, 64),
+                                              (0, 2, 16, 16, 128, 0)])
+@pytest.mark.parametrize("use_bn", [True, False])
+def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn):
+    """The fused 64-output block backward (unet_sepconv_bwd_fused) against the route it replaces:
+    unet_pointwise_bwd_data_bnrelu (dz formed on load, dy) + unet_sepconv_bwd_filter over that dz /
+    dy, and against the float64 oracle's BN + ReLU backward and weight gradients."""
+    rng = np.random.default_rng(700 + mode + n + (7 if use_bn else 0))
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C, cout, m = c0 + c1, 64, n * h * w
+    dk = dev(f32(rng.standard_normal((3, 3, C, 1))))
+    pk32 = f32(rng.standard_normal((1, 1, C, cout)) / np.sqrt(C))
+    pk = dev(pk32)
+    z = f32(rng.standard_normal((m, 1, 1, cout)) * 2 + 0.3)
+    da = f32(rng.standard_normal((m, 1, 1, cout)))
+    gamma, beta = bn_affine(rng, cout)
+    if use_bn:
+        _, mean, var = K.bn_train(z, gamma, beta)
+        rstd = 1 / np.sqrt(var + 1e-3)
+        scale, shift = f32(gamma * rstd), f32(beta - mean * gamma * rstd)
+    else:
+        mean = var = rstd = np.zeros(cout)
+        scale, shift = np.ones(cout, np.float32), f32(beta)
+    ts, th, tz, tda = dev(scale), dev(shift), dev(z), dev(da)
+    coef = torch.empty(3 * cout, device="cuda")
+    dg, db = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    ops.bn_relu_bwd_stats(tda, tz, m, cout, dev(f32(mean)), dev(f32(rstd)), ts, th, use_bn, 0.0, 0,
+                          dg if use_bn else None, db, coef)
+    v = _mk_view(ops, mode, t)
+    dy_f = torch.full((n, h, w, C), 7.0, device="cuda")
+    ddk_f, dpk_f = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
+    ops.sepconv_bwd_fused(v, n, h, w, dk, pk, tda, tz, ts, th, coef, cout, dy_f, ddk_f, dpk_f)
+    dy_r, dz_r = torch.empty((m, C), device="cuda"), torch.empty((m, cout), device="cuda")
+    ops.pointwise_bwd_data_bnrelu(tda, tz, m, C, cout, pk, ts, th, coef, 0.0, 0, dy_r, dz_r)
+    ddk_r, dpk_r = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
+    ops.sepconv_bwd_filter(v, n, h, w, dk, dy_r, dz_r, cout, ddk_r, dpk_r)
+    assert rel_err(host(dy_f).reshape(m, C), host(dy_r)) < 2e-6
+    assert rel_err(host(dpk_f), host(dpk_r)) < 2e-6
+    assert rel_err(host(ddk_f), host(ddk_r)) < 2e-6
+    # float64 oracle
+    if use_bn:
+        rz, _, _ = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var))
+    else:
+        rz = np.where(z + beta > 0, da, 0)
+    rz = rz.reshape(m, cout).astype(np.float64)
+    ry = rz @ pk32[0, 0].T.astype(np.float64)
+    assert rel_err(host(dy_f).reshape(m, C), ry) < 1e-4
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"),
+                    0.0, 0).astype(np.float64)
+    yr = K.depthwise3x3(xv, host(dk).astype(np.float64))
+    assert rel_err(host(dpk_f).reshape(C, cout), yr.reshape(m, C).T @ rz) < 1e-4

@@ -37,10 +37,15 @@ constexpr int NT = 512;                                               // threads
 constexpr int NHQ = HPIX * (CI / 4);                                  // halo float4 (2880)
 constexpr int HR = (NHQ + NT - 1) / NT;                               // per thread (6)
 constexpr int LDS_HALO = HPIX * CI, LDS_YT = 128 * CI;
-template <int CO>
+template <int CO, bool FUSED = false>
 struct SwLds {
-    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * CO;  // 110 KB (CO 64) / 142 KB (CO 128)
+    // FUSED: dz tile rows padded to CO + 1 floats (the dy MFMA reads it down a column), plus the
+    // block's pointwise kernel slice Wt [CO][64 ci] and the dy tile [128 px][64 ci]: 157.5 KB
+    static constexpr int ZS = FUSED ? CO + 1 : CO;
+    static constexpr int WT = FUSED ? CO * CI : 0, DYT = FUSED ? 128 * CI : 0, KT = FUSED ? 9 * CI : 0;
+    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * ZS + WT + DYT + KT;  // 110 KB (CO 64) / 142 KB (CO 128)
     static_assert(64 * 64 * 2 <= SIZE && 9 * 32 * 16 * 4 <= SIZE, "epilogue scratch");
+    static_assert(SIZE * 4 <= 160 * 1024, "LDS");
 };
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
@@ -55,18 +60,30 @@ struct SwArgs {
     float* dw_slab;   // [S][9][Cin]
     int tiles, tps;   // pixel tiles, tiles per m-slice
     int ncig;         // ci groups of 64 channels
+    // FUSED (the whole backward of a 64-output conv block but its depthwise data gradient): dz is
+    // formed per tile from the block's incoming gradient da and raw z exactly as the BN-backward
+    // data-gradient GEMM forms it (gemm.hip A_BNBWD), dy = dz . pk^T is computed here and written
+    // out (dy_out), and never goes through HBM as dz
+    const float *da, *z, *coef, *bsc, *bsh, *pk;
+    float* dy_out;
 };
 
-template <int MODE, bool DROP, int CO>
+template <int MODE, bool DROP, int CO, bool FUSED = false>
 __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
+    static_assert(!FUSED || CO == 64, "fused block backward: 64 output channels");
     constexpr int DQ = 128 * CO / 4 / NT;  // dz float4 per thread per tile (4 / 8)
     constexpr int NQ = 2 * (CO / 32);      // (32 ci x 32 co) quarters of the block's 64 x CO output
     constexpr int PP = 8 / NQ;             // waves per quarter (pixel parts of the tile)
     constexpr int KS = 64 / PP;            // MFMA k-steps (pixel pairs) per wave per tile
-    __shared__ __attribute__((aligned(16))) float smem[SwLds<CO>::SIZE];
+    using L = SwLds<CO, FUSED>;
+    constexpr int ZS = L::ZS;
+    __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     float* Xs = smem;
     float* Ys = smem + LDS_HALO;
     float* Zs = smem + LDS_HALO + LDS_YT;
+    float* Wt = Zs + 128 * ZS;  // FUSED: [co][ci]
+    float* DY = Wt + L::WT;     // FUSED: [px][ci]
+    float* KS9 = DY + L::DYT;   // FUSED: the 9 depthwise taps of the ci group [t][ci] (not in registers)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
     // XCD-aware block -> (ci group, m-slice): blocks b and b + 8 run on one XCD; the ci groups of
@@ -81,9 +98,13 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 
     // this thread's channel quad (halo staging, y and filter-gradient quads alike)
     const int cq = tid & 15, ci = c0 + 4 * cq;
-    float4 kt[9];
+    float4 kt[FUSED ? 1 : 9];
+    if constexpr (FUSED) {
+        for (int e = tid; e < 9 * CI; e += NT) KS9[e] = g.dk[(e / CI) * Cin + c0 + e % CI];
+    } else {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
+        for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
+    }
     const float* src = g.x.src0;
     int cs = g.x.c0, cc = ci;
     const float* scp = g.x.sc0;
@@ -107,7 +128,14 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         }
     }
 
+    if constexpr (FUSED) {
+        for (int e = tid; e < CO * CI; e += NT) {  // Wt[co][ci] = pk[c0 + ci][co]
+            const int co = e / CI, cl = e - co * CI;
+            Wt[co * CI + cl] = g.pk[(int64_t)(c0 + cl) * CO + co];
+        }
+    }
     float4 hx[HR], rz[DQ], rdy[4];
+    float4 rzz[FUSED ? DQ : 1];
     int lp[HR];
     auto load = [&](int T) {
         const int tw = T % tiles_w, r0 = T / tiles_w;
@@ -125,7 +153,13 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e / (CO/4), quad e % (CO/4)
             const int e = tid + NT * k, p = e / (CO / 4), q = e % (CO / 4);
-            rz[k] = ld4(g.dz + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q);
+            const int64_t o = (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q;
+            if constexpr (FUSED) {
+                rz[k] = ld4(g.da + o);
+                rzz[k] = ld4(g.z + o);
+            } else {
+                rz[k] = ld4(g.dz + o);
+            }
         }
     };
     auto load_dy = [&](int T) {  // dy of this thread's quads: pixel (tid >> 4) + 32 k
@@ -139,6 +173,17 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         }
     };
     auto store = [&]() {
+        // FUSED: this thread's dz quad is output-channel quad tid % 16 in every k; its BN constants
+        // are re-read here (L1 hits) rather than held in 20 registers across the tile
+        float4 fsc, fsh, fmu, fp, fq;
+        if constexpr (FUSED) {
+            const int q = 4 * (tid % (CO / 4));
+            fsc = ld4(g.bsc + q);
+            fsh = ld4(g.bsh + q);
+            fmu = ld4(g.coef + q);
+            fp = ld4(g.coef + CO + q);
+            fq = ld4(g.coef + 2 * CO + q);
+        }
 #pragma unroll
         for (int k = 0; k < HR; ++k) {
             const int e = tid + NT * k;
@@ -156,7 +201,25 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {
             const int e = tid + NT * k;
-            *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
+            if constexpr (FUSED) {  // dz = sc (g - p - (z - mu) q), g = da [z sc + sh > 0] (as gemm.hip A_BNBWD)
+                float4 v = rz[k];
+                const float4 zz = rzz[k];
+                v.x = fmaf(zz.x, fsc.x, fsh.x) > 0.f ? v.x : 0.f;
+                v.y = fmaf(zz.y, fsc.y, fsh.y) > 0.f ? v.y : 0.f;
+                v.z = fmaf(zz.z, fsc.z, fsh.z) > 0.f ? v.z : 0.f;
+                v.w = fmaf(zz.w, fsc.w, fsh.w) > 0.f ? v.w : 0.f;
+                v.x = fsc.x * (v.x - fp.x - (zz.x - fmu.x) * fq.x);
+                v.y = fsc.y * (v.y - fp.y - (zz.y - fmu.y) * fq.y);
+                v.z = fsc.z * (v.z - fp.z - (zz.z - fmu.z) * fq.z);
+                v.w = fsc.w * (v.w - fp.w - (zz.w - fmu.w) * fq.w);
+                float* d = &Zs[(e / (CO / 4)) * ZS + 4 * (e % (CO / 4))];
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
+            } else {
+                *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
+            }
         }
     };
 
@@ -173,36 +236,62 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 
     if (t_begin < t_end) {
         load(t_begin);
-        load_dy(t_begin);
+        if constexpr (!FUSED) load_dy(t_begin);
     }
     for (int T = t_begin; T < t_end; ++T) {
         if constexpr (!(SW_KO & 8)) store();
         __syncthreads();
         if constexpr (!(SW_KO & 4)) load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
+        int64_t tbase = 0;  // FUSED: the tile's first pixel (dy rows are written from the DY tile)
+        if constexpr (FUSED) {
+            // dy [128 px][64 ci] = dz [128 px][CO] . Wt [CO][64 ci]: wave w -> 32 pixels x 32 channels
+            const int px0 = 32 * (wave >> 1), cl0 = 32 * (wave & 1);
+            floatx16 ad;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ad[r] = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < CO; k += 2)
+                ad = __builtin_amdgcn_mfma_f32_32x32x2f32(Zs[(px0 + lo) * ZS + k + hi], Wt[(k + hi) * CI + cl0 + lo], ad,
+                                                          0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) DY[(px0 + acc_row(r, hi)) * CI + cl0 + lo] = ad[r];
+            const int tw = T % tiles_w, r0 = T / tiles_w;
+            tbase = (int64_t)((r0 / tiles_h) * g.H + (r0 % tiles_h) * TH) * g.W + tw * TW;
+            __syncthreads();
+        }
 #pragma unroll 1
         for (int k = 0; k < ((SW_KO & 2) ? 0 : 4); ++k) {  // (not unrolled: 9 taps in flight, not 36)
             const int p = (tid >> 4) + 32 * k, pr = p >> 4, pc = p & 15;
-            const float4 dq = rdy[0];  // static register indexing: rotate the dy quads
-            rdy[0] = rdy[1];
-            rdy[1] = rdy[2];
-            rdy[2] = rdy[3];
+            float4 dq;
+            if constexpr (FUSED) {
+                dq = *reinterpret_cast<const float4*>(&DY[p * CI + 4 * cq]);
+                st4(g.dy_out + (tbase + (int64_t)pr * g.W + pc) * Cin + ci, dq);
+            } else {
+                dq = rdy[0];  // static register indexing: rotate the dy quads
+                rdy[0] = rdy[1];
+                rdy[1] = rdy[2];
+                rdy[2] = rdy[3];
+            }
             float4 y = f4(0.f);
 #pragma unroll
             for (int dy_ = 0; dy_ < 3; ++dy_)
 #pragma unroll
                 for (int dx_ = 0; dx_ < 3; ++dx_) {
                     const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
-                    y = fma4(xv, kt[dy_ * 3 + dx_], y);
+                    if constexpr (FUSED)
+                        y = fma4(xv, *reinterpret_cast<const float4*>(&KS9[(dy_ * 3 + dx_) * CI + 4 * cq]), y);
+                    else
+                        y = fma4(xv, kt[dy_ * 3 + dx_], y);
                     dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
                 }
             *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
         }
-        if constexpr (!(SW_KO & 4)) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
+        if constexpr (!(SW_KO & 4) && !FUSED) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
         __syncthreads();
 #pragma unroll 4
         for (int s = 0; s < ((SW_KO & 1) ? 0 : KS); ++s) {
             const int p = wpx + 2 * s + hi;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[p * CI + wci + lo], Zs[p * CO + wco + lo], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[p * CI + wci + lo], Zs[p * ZS + wco + lo], acc, 0, 0, 0);
         }
         __syncthreads();
     }
@@ -265,7 +354,8 @@ SwPlan sw_plan(int n, int h, int w, int cin) {
 
 template <int MODE, bool DROP>
 void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
-    if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
+    if (a.da) sepconv_wgrad_kernel<MODE, false, 64, true><<<blocks, NT, 0, st>>>(a);
+    else if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
     else sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
 }
 
@@ -294,30 +384,19 @@ extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin
     return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
 }
 
-extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                                       const float* dy, const float* dz, int cout, float* d_dw_kernel,
-                                       float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
-    if (check_view(x, "unet_sepconv_bwd_filter")) return -1;
-    UNET_CHECK_ARG(unet_sepconv_bwd_filter_supported(x, n, h, w, cout),
-                   "unet_sepconv_bwd_filter: unsupported shape (needs input channels %% 64 == 0, 64 or 128 "
-                   "output channels, a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
-    UNET_CHECK_ARG(dw_kernel && dy && dz && d_dw_kernel && d_pw_kernel, "unet_sepconv_bwd_filter: null pointer");
-    UNET_CHECK_ARG(((uintptr_t)dy | (uintptr_t)dz | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
-                    (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
-                   "unet_sepconv_bwd_filter: operands must be 16-B aligned");
+namespace {
+int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwArgs a, int cout, float* d_dw_kernel,
+           float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream, const char* op) {
     const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
-    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_sepconv_bwd_filter: workspace %zu < %zu", ws_bytes, need);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
     const SwPlan p = sw_plan(n, h, w, cin);
-    SwArgs a{};
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;
     a.W = w;
     a.Cin = cin;
     a.dk = dw_kernel;
-    a.dy = dy;
-    a.dz = dz;
     a.pw_slab = static_cast<float*>(ws);
     a.dw_slab = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)p.S * cin * cout * sizeof(float), 256));
     a.tiles = p.tiles;
@@ -340,9 +419,54 @@ extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, 
             else launch_sw<UNET_VIEW_CONCAT, false>(a, cout, blocks, st);
             break;
     }
-    UNET_CHECK_LAUNCH("unet_sepconv_bwd_filter");
+    UNET_CHECK_LAUNCH(op);
     const int64_t lp = (int64_t)cin * cout, ld = (int64_t)9 * cin;
     int rc = reduce_slabs(a.pw_slab, p.S, lp, d_pw_kernel, lp, lp, st);
     if (rc) return rc;
     return reduce_slabs(a.dw_slab, p.S, ld, d_dw_kernel, ld, ld, st);
+}
+}  // namespace
+
+extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                                      const float* pw_kernel, const float* da, const float* z, const float* scale,
+                                      const float* shift, const float* coef, int cout, float* dy, float* d_dw_kernel,
+                                      float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    const char* op = "unet_sepconv_bwd_fused";
+    if (check_view(x, op)) return -1;
+    UNET_CHECK_ARG(cout == 64 && unet_sepconv_bwd_filter_supported(x, n, h, w, cout) && x->drop_rate == 0.f,
+                   "%s: unsupported (needs 64 output channels, input channels %% 64 == 0, no dropout on the input, "
+                   "a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)", op);
+    UNET_CHECK_ARG(dw_kernel && pw_kernel && da && z && scale && shift && coef && dy && d_dw_kernel && d_pw_kernel,
+                   "%s: null pointer", op);
+    UNET_CHECK_ARG(((uintptr_t)da | (uintptr_t)z | (uintptr_t)dy | (uintptr_t)scale | (uintptr_t)shift |
+                    (uintptr_t)coef | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
+                    (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
+                   "%s: operands must be 16-B aligned", op);
+    SwArgs a{};
+    a.da = da;
+    a.z = z;
+    a.coef = coef;
+    a.bsc = scale;
+    a.bsh = shift;
+    a.pk = pw_kernel;
+    a.dy_out = dy;
+    return run_sw(x, n, h, w, dw_kernel, a, cout, d_dw_kernel, d_pw_kernel, ws, ws_bytes, stream, op);
+}
+
+extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                                       const float* dy, const float* dz, int cout, float* d_dw_kernel,
+                                       float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    if (check_view(x, "unet_sepconv_bwd_filter")) return -1;
+    UNET_CHECK_ARG(unet_sepconv_bwd_filter_supported(x, n, h, w, cout),
+                   "unet_sepconv_bwd_filter: unsupported shape (needs input channels %% 64 == 0, 64 or 128 "
+                   "output channels, a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)");
+    UNET_CHECK_ARG(dw_kernel && dy && dz && d_dw_kernel && d_pw_kernel, "unet_sepconv_bwd_filter: null pointer");
+    UNET_CHECK_ARG(((uintptr_t)dy | (uintptr_t)dz | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
+                    (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
+                   "unet_sepconv_bwd_filter: operands must be 16-B aligned");
+    SwArgs a{};
+    a.dy = dy;
+    a.dz = dz;
+    return run_sw(x, n, h, w, dw_kernel, a, cout, d_dw_kernel, d_pw_kernel, ws, ws_bytes, stream,
+                  "unet_sepconv_bwd_filter");
 }

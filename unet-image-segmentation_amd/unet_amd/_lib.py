@@ -67,6 +67,8 @@ SIGNATURES = {
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_int, P, P, P, c_size_t, P]),
+    "unet_sepconv_bwd_fused": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, c_int, P, P, P, P, c_size_t,
+                                       P]),
     "unet_sepconv_set_schedule": (c_int, [c_int]),
     "unet_bn_finalize": (c_int, [P, c_int64, c_int, P, P, c_float, c_float, P, P, c_int, P, P, P, P, P]),
     "unet_bn_infer_params": (c_int, [P, P, P, P, c_int, c_float, P, P, P]),

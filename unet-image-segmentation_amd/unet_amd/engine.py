@@ -181,6 +181,11 @@ class UNetEngine:
         # finish, instead of beside its own depthwise data gradient (under data parallelism the
         # all-reduce low-water report waits for the deferred launch, see _grads_ready)
         self.defer_sw = os.environ.get("UNET_SW_DEFER", "1") != "0"
+        # the y-recomputing 64-output blocks run their whole backward but the depthwise data
+        # gradient as ONE main-stream pass (unet_sepconv_bwd_fused: dz formed per tile, dy and both
+        # weight gradients from it; dz never stored) instead of the data-gradient GEMM + the
+        # side-stream weight-gradient pass
+        self.fuse_block_bwd = True
         self._pending_side = None
         self._pending_ready: Optional[str] = None
         self._ev = None  # created on first use (on the device)
@@ -531,6 +536,8 @@ class UNetEngine:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
         dk, pk = self._wts(b, refresh=False)
         img_wg = False
+        fused_bwd = self.fuse_block_bwd and self.fuse_bn_bwd and bb.y_recompute and drop_rate == 0.0 and \
+            b.cout == 64
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
             if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
@@ -546,6 +553,10 @@ class UNetEngine:
             if img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
                 ops.pointwise_bwd_data_bnrelu_wgrad(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                                     bb.y, dy, self._gwts(b)[1])
+            elif fused_bwd:  # dy and both weight gradients in one pass over (da, z, the input view)
+                gdk_f, gpk_f = self._gwts(b)
+                ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, bb.da, bb.z, bb.scale, bb.shift, bb.coef, b.cout, dy,
+                                      gdk_f, gpk_f)
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, dz)
@@ -556,6 +567,8 @@ class UNetEngine:
         gdk, gpk = self._gwts(b)
 
         def weight_grads():
+            if fused_bwd:  # (done by the fused pass)
+                return
             if bb.y_recompute:  # both kernels' gradients in one pass, y recomputed from view_in
                 ops.sepconv_bwd_filter(view_f, n, h, w, dk, dy, dz, b.cout, gdk, gpk)
                 return
@@ -569,7 +582,9 @@ class UNetEngine:
 
         # the image block (dx0 None) has no data gradient after this: its weight gradients run
         # on the otherwise idle main stream, beside the side stream's enc1_block2 tail
-        if self.overlap and dx0 is not None:
+        if fused_bwd:
+            pass
+        elif self.overlap and dx0 is not None:
             self._flush_side()
             if self.defer_sw and bb.y_recompute:
                 self._pending_side = weight_grads

@@ -401,6 +401,28 @@ def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> 
     return bool(L.load().unet_sepconv_bwd_filter_supported(ctypes.byref(vs), n, h, w, cout))
 
 
+def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, da: Tensor, z: Tensor, scale: Tensor,
+                      shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Tensor, dpk: Tensor):
+    """A 64-output block's BN + ReLU backward, pointwise data gradient and both weight gradients
+    in one pass (dz never stored): dy out, d_depthwise / d_pointwise kernels overwritten."""
+    C = x.channels
+    m = n * h * w
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(pk, "pointwise_kernel", C * cout)
+    _check(da, "da", m * cout)
+    _check(z, "z", m * cout)
+    _check(coef, "coef", 3 * cout)
+    _check(dy, "dy", m * C)
+    _check(ddk, "d_depthwise_kernel", 9 * C)
+    _check(dpk, "d_pointwise_kernel", C * cout)
+    ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
+    vs = x.c_struct()
+    _call("unet_sepconv_bwd_fused", (4.0 * m * C * cout + 36.0 * m * C,
+                                     x.src_bytes(n, h, w) + 4.0 * (m * C + 2 * m * cout)),
+          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(pk), _ptr(da), _ptr(z), _ptr(scale), _ptr(shift), _ptr(coef), cout,
+          _ptr(dy), _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
+
+
 def sepconv_bwd_filter(x: View, n: int, h: int, w: int, dk: Tensor, dy: Tensor, dz: Tensor, cout: int,
                        ddk: Tensor, dpk: Tensor):
     """Depthwise and pointwise kernel gradients in one pass, y recomputed from the view x."""
