@@ -1,5 +1,7 @@
 """Run the fused sepconv forward (or the split dw + pw pair) on one shape repeatedly, for
-rocprofv3 --pmc passes.  usage: sep_one.py MODE H W CIN COUT [iters] [split]"""
+rocprofv3 --pmc passes.  usage: sep_one.py MODE H W CIN COUT [iters] [split|x3]   (N images: env N,
+default 16; x3 = the split-precision variant with pre-split weight planes, as the train step runs
+it at channels % 16 == 0)"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "unet-image-segmentation_amd"), ROOT]
@@ -7,8 +9,8 @@ import torch
 from unet_amd import ops
 mode, h, w, C, cout = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
-split = len(sys.argv) > 7 and sys.argv[7] == "split"
-N = 16
+opt = sys.argv[7] if len(sys.argv) > 7 else ""
+N = int(os.environ.get("N", 16))
 big = 2 if mode == 2 else 1
 src = torch.randn(N, big * h, big * w, C, device="cuda")
 sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
@@ -16,13 +18,17 @@ v = ops.View.plain(src) if mode == 0 else (ops.View.pool_bnrelu(src, sc, sh) if 
 m = N * h * w
 dk = torch.randn(3, 3, C, 1, device="cuda")
 pk = torch.randn(1, 1, C, cout, device="cuda") * 0.05
+pkx = None
+if opt == "x3":
+    pkx = torch.empty(3 * C * cout, dtype=torch.int16, device="cuda")
+    ops.split_x3(pk, [(0, C, cout, 0)], pkx)
 y = torch.empty(N, h, w, C, device="cuda")
 z = torch.empty(N, h, w, cout, device="cuda")
 part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
 for _ in range(iters):
-    if split:
+    if opt == "split":
         ops.dwconv3x3_fwd(v, N, h, w, dk, y)
         ops.pointwise_fwd(y, m, C, cout, pk, z, part)
     else:
-        ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part)
+        ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part, pkx=pkx)
 torch.cuda.synchronize()
