@@ -38,10 +38,12 @@ def main():
                              text=True).stdout
         open(os.path.join(P, f"{tag}_step_trace.txt"), "w").write(out)
     fe, wr = one(f"pmc/**/{tag}_fetch_counter_collection.csv"), one(f"pmc/**/{tag}_write_counter_collection.csv")
-    if fe and wr:
-        op = "unet_pointwise_bwd_data_bnrelu"
-        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), fe, wr,
-                        os.path.join(P, f"{tag}_traffic_{op[5:]}.json"), op], check=True)
+    if fe and wr:  # the bench line's roofline op (the largest share of the single-stream breakdown), and the GEMM
+        ops_ = [json.loads(lines[0])["roofline"]["kernel"], "unet_pointwise_bwd_data_bnrelu"]
+        for op in dict.fromkeys(ops_):
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), fe, wr,
+                                os.path.join(P, f"{tag}_traffic_{op[5:]}.json"), op], capture_output=True, text=True)
+            print(op, r.stdout.strip()[:200], r.stderr.strip()[-200:])
     # enc2_block1 forward at batch 32: bytes and the SQ stall group, averaged over its dispatches
     rec = {}
     for kind in ("fetch", "write", "sq"):
