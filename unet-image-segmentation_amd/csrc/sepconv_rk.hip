@@ -39,9 +39,11 @@ struct RkLds {
     // X6: B as three bf16 planes [BN][16 k] (32-byte rows; the two 16-byte k chunks of row n are
     // swapped when bit 3 of n is set, so the fragment reads of 16-lane groups are conflict-free)
     static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = X6 ? 3 * BN * BK / 2 : BK * (BN + 4);
-    static constexpr int RING = 3 * (XSZ + KSZ + BSZ);
-    static constexpr int TLD = BN + 4;                 // epilogue transpose row stride
-    static constexpr int EPI = 4 * 32 * TLD + 4 * BN;  // 4 waves' tiles + the statistics combine
+    static constexpr int SLOTS = X6 ? 2 : 3;           // X6: two slots (53 KB: 3 blocks per CU)
+    static constexpr int RING = SLOTS * (XSZ + KSZ + BSZ);
+    static constexpr int EC = X6 && BN > 64 ? 64 : BN;  // accumulator columns per epilogue pass
+    static constexpr int TLD = EC + 4;                  // epilogue transpose row stride
+    static constexpr int EPI = 4 * 32 * TLD + 4 * BN;   // 4 waves' tiles + the statistics combine
     static constexpr int SIZE = RING > EPI ? RING : EPI;
 };
 
@@ -51,7 +53,7 @@ struct RkLds {
 // (common.h split4) and runs mfma_x6 against the pre-split weight planes (SepArgs::pkx) per 32-column
 // tile: 6 x 32 MFMA cycles per stage and tile instead of 8 x 64.
 template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y, bool X6 = false>
-__global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
+__global__ __launch_bounds__(256, X6 ? 3 : 2) void sepconv_rk_kernel(SepArgs g) {
     static_assert(!X6 || MODE != UNET_VIEW_POOL_BNRELU, "X6: no max-pool views");
     constexpr int TN = BN / 32;                 // MFMA tiles per wave (all BN columns)
     constexpr int NH = HPIX * (BK / 4);         // halo float4 per stage (720)
@@ -64,8 +66,8 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     using L = RkLds<BN, X6>;
     __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     auto Xs = [&](int b) { return smem + b * L::XSZ; };
-    auto Ks = [&](int b) { return smem + 3 * L::XSZ + b * L::KSZ; };
-    auto Bs = [&](int b) { return smem + 3 * (L::XSZ + L::KSZ) + b * L::BSZ; };
+    auto Ks = [&](int b) { return smem + L::SLOTS * L::XSZ + b * L::KSZ; };
+    auto Bs = [&](int b) { return smem + L::SLOTS * (L::XSZ + L::KSZ) + b * L::BSZ; };
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
@@ -288,19 +290,21 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
         };
         float* yrow8 = nullptr;
         if constexpr (WRITE_Y) yrow8 = g.y + ((int64_t)(n * g.H + h0 + pr) * g.W + w0 + pc) * Cin + 8 * hi;
+        // stage kt computes from slot kt % 2 while stage kt + 1's loads (issued before it) land;
+        // they are written to the other slot after the compute, then stage kt + 2's are issued.
+        // Only stage 0's loads are exposed (one latency per block, not two: at 4-8 stages per
+        // block that is most of the prologue)
         load_halo(0);
         load_bx(0);
         store_halo(0);
         store_bx(0);
-        load_halo(BK);
-        load_bx(BK);
-        store_halo(1);
-        store_bx(1);
+        if (nk > 1) {
+            load_halo(BK);
+            load_bx(BK);
+        }
         __syncthreads();
         for (int kt = 0; kt < nk; ++kt) {
-            const int cb = kt % 3, wb = (kt + 2) % 3;
-            load_halo((kt + 2) * BK);
-            load_bx((kt + 2) * BK);
+            const int cb = kt & 1, wb = cb ^ 1;
             // this stage's depthwise (VALU), then its MFMAs: with two waves per SIMD one wave's
             // depthwise runs beside the other's MFMAs (a look-ahead inside the wave needed ~60 more
             // registers and spilled)
@@ -331,9 +335,13 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
                     bfr[pl] = *reinterpret_cast<const bf16x8*>(Bb + (pl * BN + nn) * BK + 8 * cs);
                 acc[tn] = mfma_x6(af, bfr, acc[tn]);
             }
-            if (kt + 2 < nk) {
+            if (kt + 1 < nk) {
                 store_halo(wb);
                 store_bx(wb);
+                if (kt + 2 < nk) {
+                    load_halo((kt + 2) * BK);
+                    load_bx((kt + 2) * BK);
+                }
             }
             __syncthreads();
         }
@@ -374,14 +382,11 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
     }
 
     // ---- epilogue (the loop ended on a barrier: the ring is free).  Accumulator row
-    // acc_row(r, hi) of wave w is tile pixel (2w + (row >> 4), rk_col(row)).
-    constexpr int TLD = L::TLD;
+    // acc_row(r, hi) of wave w is tile pixel (2w + (row >> 4), rk_col(row)).  The accumulator
+    // tile leaves through LDS in EC-column passes (X6: 64, so the epilogue fits the two-slot ring)
+    constexpr int EC = L::EC, TLD = L::TLD;
     float* T = smem + wave * 32 * TLD;
     float* red = smem + 4 * 32 * TLD;
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) T[acc_row(r, hi) * TLD + tn * 32 + lo] = acc[tn][r];
     if constexpr (EPI == E_STATS) {
         // per column (mean, M2) of the tile's 128 rows: per-wave sums, a fixed-order combine of
         // the 4 waves through LDS
@@ -423,43 +428,51 @@ __global__ __launch_bounds__(256, 2) void sepconv_rk_kernel(SepArgs g) {
                         make_float2(mean[tn], (red[cl] + red[BN + cl]) + (red[2 * BN + cl] + red[3 * BN + cl]));
             }
         }
-    } else {
-        __syncthreads();
     }
-    // z: the wave's 32 pixels x BN channels as float4s (BN / 4 per pixel, 64 per instruction)
-    constexpr int Q4 = BN / 4, NS = 32 * Q4 / 64;
-    if (g.zsel) {
-        // the wave's two pixel rows hold 8 whole 2x2 windows: their pooling selection (zsel) for
-        // the next stage's max-pool view.  T row of pixel (sub, col): col, or 16 + ((col + 2) & 15)
-        // on the second row (rk_col's rotation inverted)
-        constexpr int NP4 = 8 * Q4 / 64;
+    constexpr int Q4 = EC / 4, NS = 32 * Q4 / 64;
 #pragma unroll
-        for (int i = 0; i < NP4; ++i) {
-            const int idx = i * 64 + lane, j = idx / Q4, q = idx - j * Q4;
-            const int c0 = 2 * j, c1 = 2 * j + 1;
-            const float4 a = *reinterpret_cast<const float4*>(&T[c0 * TLD + 4 * q]);
-            const float4 b = *reinterpret_cast<const float4*>(&T[c1 * TLD + 4 * q]);
-            const float4 c = *reinterpret_cast<const float4*>(&T[(16 + ((c0 + 2) & 15)) * TLD + 4 * q]);
-            const float4 d = *reinterpret_cast<const float4*>(&T[(16 + ((c1 + 2) & 15)) * TLD + 4 * q]);
-            const int col = n0 + 4 * q;
-            if (col < g.Cout) {
-                const float4 gm = g.gamma ? ld4(g.gamma + col) : f4(0.f);
-                float4 o;
-                o.x = pool_sel(a.x, b.x, c.x, d.x, signbit(gm.x));
-                o.y = pool_sel(a.y, b.y, c.y, d.y, signbit(gm.y));
-                o.z = pool_sel(a.z, b.z, c.z, d.z, signbit(gm.z));
-                o.w = pool_sel(a.w, b.w, c.w, d.w, signbit(gm.w));
-                const int H2 = g.H >> 1, W2 = g.W >> 1;
-                st4(g.zsel + ((int64_t)(n * H2 + (h0 >> 1) + wave) * W2 + (w0 >> 1) + j) * g.Cout + col, o);
+    for (int hp = 0; hp < BN / EC; ++hp) {
+        const int cbase = n0 + hp * EC;  // first output channel of this pass
+        __syncthreads();                 // (the statistics' / previous pass's LDS reads are done)
+#pragma unroll
+        for (int tn = 0; tn < EC / 32; ++tn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) T[acc_row(r, hi) * TLD + tn * 32 + lo] = acc[hp * (EC / 32) + tn][r];
+        __syncthreads();
+        if (g.zsel) {
+            // the wave's two pixel rows hold 8 whole 2x2 windows: their pooling selection (zsel) for
+            // the next stage's max-pool view.  T row of pixel (sub, col): col, or 16 + ((col + 2) & 15)
+            // on the second row (rk_col's rotation inverted)
+            constexpr int NP4 = 8 * Q4 / 64;
+#pragma unroll
+            for (int i = 0; i < NP4; ++i) {
+                const int idx = i * 64 + lane, j = idx / Q4, q = idx - j * Q4;
+                const int c0 = 2 * j, c1 = 2 * j + 1;
+                const float4 a = *reinterpret_cast<const float4*>(&T[c0 * TLD + 4 * q]);
+                const float4 b = *reinterpret_cast<const float4*>(&T[c1 * TLD + 4 * q]);
+                const float4 c = *reinterpret_cast<const float4*>(&T[(16 + ((c0 + 2) & 15)) * TLD + 4 * q]);
+                const float4 d = *reinterpret_cast<const float4*>(&T[(16 + ((c1 + 2) & 15)) * TLD + 4 * q]);
+                const int col = cbase + 4 * q;
+                if (col < g.Cout) {
+                    const float4 gm = g.gamma ? ld4(g.gamma + col) : f4(0.f);
+                    float4 o;
+                    o.x = pool_sel(a.x, b.x, c.x, d.x, signbit(gm.x));
+                    o.y = pool_sel(a.y, b.y, c.y, d.y, signbit(gm.y));
+                    o.z = pool_sel(a.z, b.z, c.z, d.z, signbit(gm.z));
+                    o.w = pool_sel(a.w, b.w, c.w, d.w, signbit(gm.w));
+                    const int H2 = g.H >> 1, W2 = g.W >> 1;
+                    st4(g.zsel + ((int64_t)(n * H2 + (h0 >> 1) + wave) * W2 + (w0 >> 1) + j) * g.Cout + col, o);
+                }
             }
         }
-    }
+        // z: the wave's 32 pixels x EC channels as float4s (EC / 4 per pixel, 64 per instruction)
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        const int idx = i * 64 + lane, row = idx / Q4, q = idx - row * Q4;
-        const float4 v = *reinterpret_cast<const float4*>(&T[row * TLD + 4 * q]);
-        const int ph = h0 + 2 * wave + (row >> 4), pw = w0 + rk_col(row);
-        if (n0 + 4 * q < g.Cout) st4(g.z + ((int64_t)(n * g.H + ph) * g.W + pw) * g.Cout + n0 + 4 * q, v);
+        for (int i = 0; i < NS; ++i) {
+            const int idx = i * 64 + lane, row = idx / Q4, q = idx - row * Q4;
+            const float4 v = *reinterpret_cast<const float4*>(&T[row * TLD + 4 * q]);
+            const int ph = h0 + 2 * wave + (row >> 4), pw = w0 + rk_col(row);
+            if (cbase + 4 * q < g.Cout) st4(g.z + ((int64_t)(n * g.H + ph) * g.W + pw) * g.Cout + cbase + 4 * q, v);
+        }
     }
 }
 
