@@ -186,8 +186,10 @@ int unet_pool_select(const float* z, int n, int h, int w, int c, const float* ga
                      float* out, unet_stream_t stream);
 /* Kernel schedule of unet_sepconv_fwd (process-wide; returns the previous value, < 0 on a bad
  * value).  AUTO: the register-A kernel (each lane computes the depthwise output straight in the
- * MFMA operand layout) for BN+ReLU / concat / plain views of >= 64 channels, the LDS-A-tile
- * kernel otherwise.  TILE / RK force one (RK fails with -1 where it does not exist): both are
+ * MFMA operand layout) for BN+ReLU / concat / plain views of >= 64 input and output channels
+ * and for max-pool views of >= 64 inputs and 64..128 outputs; the LDS-A-tile kernel otherwise
+ * (max-pool views of > 128 outputs: its 256-wide tile pools each halo element once for all
+ * columns).  TILE / RK force one (RK fails with -1 where it does not exist): both are
  * parity-tested (tests/test_ops_gpu.py).  Identical results: both form each output as the
  * same k-ordered fmaf chain.                                                                  */
 enum { UNET_SEPCONV_AUTO = 0, UNET_SEPCONV_TILE = 1, UNET_SEPCONV_RK = 2 };

@@ -467,9 +467,10 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     a.gamma = gamma;
     UNET_CHECK_ARG(((uintptr_t)pw_kernel_x3 & 15) == 0, "unet_sepconv_fwd: pw_kernel_x3 must be 16-B aligned");
     a.pkx = pw_kernel_x3;
-    // register-A schedule where it exists (BN+ReLU / concat / plain views, >= 64 channels) unless
-    // the LDS-A-tile schedule is forced; max-pool views keep the LDS-A-tile kernel (4 raw loads
-    // per halo element need its wider 8-wave staging)
+    // register-A schedule where it exists (rk_supported: BN+ReLU / concat / plain views of >= 64
+    // channels, max-pool views of >= 64 inputs and <= 128 outputs) unless the LDS-A-tile schedule
+    // is forced; wider max-pool views keep the LDS-A-tile kernel (its 256-wide 8-wave tile pools
+    // each halo element once for all columns)
     if (g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout)) {
         if (launch_rk(a, x->mode, drop, stats, wy, st)) return -1;
         UNET_CHECK_LAUNCH("unet_sepconv_fwd");

@@ -210,7 +210,9 @@ class UNetModel:
         """Data parallel: average the BatchNorm moving statistics over the ranks (tf.distribute
         keeps them sync-on-read MEAN; the moving update is linear, so averaging at any point
         leaves the mean's trajectory unchanged).  Called before validation and so before every
-        checkpoint; a no-op on one process."""
+        checkpoint; a no-op on one process.  A custom loop that calls train_step directly must
+        call it on EVERY rank (it is a collective) before save_weights / predict / evaluate, or
+        each rank keeps its own moving statistics."""
         from .dp import average_
         if self.bucketer is not None and self.bucketer.world > 1:
             average_(self.engine.stats, self.bucketer.group)
