@@ -22,13 +22,17 @@
 //     pixels (A = y^T, B = dz: one conflict-free ds_read_b32 each per MFMA).
 // The two pixel halves of each quarter and the 32 threads per channel quad of the filter gradient
 // are combined in fixed order; one slab per block, reduced by reduce_slabs in fixed order.
+// The train step runs the fused block backward further down (sepconv_bwd_fused_kernel) instead of
+// this kernel; unet_sepconv_bwd_filter stays in the ABI (tested, and the route for a caller that
+// has dz and dy already).
 #include "common.h"
 #include "view.h"
 
 namespace unet {
 namespace {
 
-#ifndef SW_KO  // lab knock-outs (tools/lab/sw_lab.hip): 1 MFMA, 2 depthwise VALU, 4 loop loads, 8 LDS staging
+#ifndef SW_KO  // lab knock-outs (tools/lab/sw_lab.hip, sw_fused_lab.hip): 1 MFMA, 2 depthwise VALU, 4 loop loads,
+               // 8 LDS staging, 16 the fused dy GEMM, 32 the fused dy store
 #define SW_KO 0
 #endif
 constexpr int TH = 8, TW = 16, HWp = TW + 2, HPIX = (TH + 2) * HWp;  // 180 halo pixels
@@ -37,13 +41,9 @@ constexpr int NT = 512;                                               // threads
 constexpr int NHQ = HPIX * (CI / 4);                                  // halo float4 (2880)
 constexpr int HR = (NHQ + NT - 1) / NT;                               // per thread (6)
 constexpr int LDS_HALO = HPIX * CI, LDS_YT = 128 * CI;
-template <int CO, bool FUSED = false>
+template <int CO>
 struct SwLds {
-    // FUSED: dz tile rows padded to CO + 1 floats (the dy MFMA reads it down a column), plus the
-    // block's pointwise kernel slice Wt [CO][64 ci] and the dy tile [128 px][64 ci]: 157.5 KB
-    static constexpr int ZS = FUSED ? CO + 1 : CO;
-    static constexpr int WT = FUSED ? CO * CI : 0, DYT = FUSED ? 128 * CI : 0, KT = FUSED ? 9 * CI : 0;
-    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * ZS + WT + DYT + KT;  // 110 KB (CO 64) / 142 KB (CO 128)
+    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * CO;  // 110 KB (CO 64) / 142 KB (CO 128)
     static_assert(64 * 64 * 2 <= SIZE && 9 * 32 * 16 * 4 <= SIZE, "epilogue scratch");
     static_assert(SIZE * 4 <= 160 * 1024, "LDS");
 };
@@ -60,30 +60,26 @@ struct SwArgs {
     float* dw_slab;   // [S][9][Cin]
     int tiles, tps;   // pixel tiles, tiles per m-slice
     int ncig;         // ci groups of 64 channels
-    // FUSED (the whole backward of a 64-output conv block but its depthwise data gradient): dz is
-    // formed per tile from the block's incoming gradient da and raw z exactly as the BN-backward
-    // data-gradient GEMM forms it (gemm.hip A_BNBWD), dy = dz . pk^T is computed here and written
-    // out (dy_out), and never goes through HBM as dz
+    // fused block backward (sepconv_bwd_fused_kernel: the whole backward of a 64-output conv block
+    // but its depthwise data gradient): dz is formed per tile from the block's incoming gradient da
+    // and raw z exactly as the BN-backward data-gradient GEMM forms it (gemm.hip A_BNBWD), dy =
+    // dz . pk^T is computed there and written out (dy_out), and never goes through HBM as dz
     const float *da, *z, *coef, *bsc, *bsh, *pk;
     float* dy_out;
 };
 
-template <int MODE, bool DROP, int CO, bool FUSED = false>
+template <int MODE, bool DROP, int CO>
 __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
-    static_assert(!FUSED || CO == 64, "fused block backward: 64 output channels");
     constexpr int DQ = 128 * CO / 4 / NT;  // dz float4 per thread per tile (4 / 8)
     constexpr int NQ = 2 * (CO / 32);      // (32 ci x 32 co) quarters of the block's 64 x CO output
     constexpr int PP = 8 / NQ;             // waves per quarter (pixel parts of the tile)
     constexpr int KS = 64 / PP;            // MFMA k-steps (pixel pairs) per wave per tile
-    using L = SwLds<CO, FUSED>;
-    constexpr int ZS = L::ZS;
+    using L = SwLds<CO>;
+    constexpr int ZS = CO;
     __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     float* Xs = smem;
     float* Ys = smem + LDS_HALO;
     float* Zs = smem + LDS_HALO + LDS_YT;
-    float* Wt = Zs + 128 * ZS;  // FUSED: [co][ci]
-    float* DY = Wt + L::WT;     // FUSED: [px][ci]
-    float* KS9 = DY + L::DYT;   // FUSED: the 9 depthwise taps of the ci group [t][ci] (not in registers)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
     // XCD-aware block -> (ci group, m-slice): blocks b and b + 8 run on one XCD; the ci groups of
@@ -98,13 +94,9 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 
     // this thread's channel quad (halo staging, y and filter-gradient quads alike)
     const int cq = tid & 15, ci = c0 + 4 * cq;
-    float4 kt[FUSED ? 1 : 9];
-    if constexpr (FUSED) {
-        for (int e = tid; e < 9 * CI; e += NT) KS9[e] = g.dk[(e / CI) * Cin + c0 + e % CI];
-    } else {
+    float4 kt[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
-    }
+    for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
     const float* src = g.x.src0;
     int cs = g.x.c0, cc = ci;
     const float* scp = g.x.sc0;
@@ -128,14 +120,7 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         }
     }
 
-    if constexpr (FUSED) {
-        for (int e = tid; e < CO * CI; e += NT) {  // Wt[co][ci] = pk[c0 + ci][co]
-            const int co = e / CI, cl = e - co * CI;
-            Wt[co * CI + cl] = g.pk[(int64_t)(c0 + cl) * CO + co];
-        }
-    }
     float4 hx[HR], rz[DQ], rdy[4];
-    float4 rzz[FUSED ? DQ : 1];
     int lp[HR];
     auto load = [&](int T) {
         const int tw = T % tiles_w, r0 = T / tiles_w;
@@ -154,12 +139,7 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e / (CO/4), quad e % (CO/4)
             const int e = tid + NT * k, p = e / (CO / 4), q = e % (CO / 4);
             const int64_t o = (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q;
-            if constexpr (FUSED) {
-                rz[k] = ld4(g.da + o);
-                rzz[k] = ld4(g.z + o);
-            } else {
-                rz[k] = ld4(g.dz + o);
-            }
+            rz[k] = ld4(g.dz + o);
         }
     };
     auto load_dy = [&](int T) {  // dy of this thread's quads: pixel (tid >> 4) + 32 k
@@ -173,17 +153,6 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
         }
     };
     auto store = [&]() {
-        // FUSED: this thread's dz quad is output-channel quad tid % 16 in every k; its BN constants
-        // are re-read here (L1 hits) rather than held in 20 registers across the tile
-        float4 fsc, fsh, fmu, fp, fq;
-        if constexpr (FUSED) {
-            const int q = 4 * (tid % (CO / 4));
-            fsc = ld4(g.bsc + q);
-            fsh = ld4(g.bsh + q);
-            fmu = ld4(g.coef + q);
-            fp = ld4(g.coef + CO + q);
-            fq = ld4(g.coef + 2 * CO + q);
-        }
 #pragma unroll
         for (int k = 0; k < HR; ++k) {
             const int e = tid + NT * k;
@@ -201,25 +170,7 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {
             const int e = tid + NT * k;
-            if constexpr (FUSED) {  // dz = sc (g - p - (z - mu) q), g = da [z sc + sh > 0] (as gemm.hip A_BNBWD)
-                float4 v = rz[k];
-                const float4 zz = rzz[k];
-                v.x = fmaf(zz.x, fsc.x, fsh.x) > 0.f ? v.x : 0.f;
-                v.y = fmaf(zz.y, fsc.y, fsh.y) > 0.f ? v.y : 0.f;
-                v.z = fmaf(zz.z, fsc.z, fsh.z) > 0.f ? v.z : 0.f;
-                v.w = fmaf(zz.w, fsc.w, fsh.w) > 0.f ? v.w : 0.f;
-                v.x = fsc.x * (v.x - fp.x - (zz.x - fmu.x) * fq.x);
-                v.y = fsc.y * (v.y - fp.y - (zz.y - fmu.y) * fq.y);
-                v.z = fsc.z * (v.z - fp.z - (zz.z - fmu.z) * fq.z);
-                v.w = fsc.w * (v.w - fp.w - (zz.w - fmu.w) * fq.w);
-                float* d = &Zs[(e / (CO / 4)) * ZS + 4 * (e % (CO / 4))];
-                d[0] = v.x;
-                d[1] = v.y;
-                d[2] = v.z;
-                d[3] = v.w;
-            } else {
-                *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
-            }
+            *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
         }
     };
 
@@ -236,57 +187,31 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
 
     if (t_begin < t_end) {
         load(t_begin);
-        if constexpr (!FUSED) load_dy(t_begin);
+        load_dy(t_begin);
     }
     for (int T = t_begin; T < t_end; ++T) {
         if constexpr (!(SW_KO & 8)) store();
         __syncthreads();
         if constexpr (!(SW_KO & 4)) load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
-        int64_t tbase = 0;  // FUSED: the tile's first pixel (dy rows are written from the DY tile)
-        if constexpr (FUSED) {
-            // dy [128 px][64 ci] = dz [128 px][CO] . Wt [CO][64 ci]: wave w -> 32 pixels x 32 channels
-            const int px0 = 32 * (wave >> 1), cl0 = 32 * (wave & 1);
-            floatx16 ad;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) ad[r] = 0.f;
-#pragma unroll 8
-            for (int k = 0; k < CO; k += 2)
-                ad = __builtin_amdgcn_mfma_f32_32x32x2f32(Zs[(px0 + lo) * ZS + k + hi], Wt[(k + hi) * CI + cl0 + lo], ad,
-                                                          0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) DY[(px0 + acc_row(r, hi)) * CI + cl0 + lo] = ad[r];
-            const int tw = T % tiles_w, r0 = T / tiles_w;
-            tbase = (int64_t)((r0 / tiles_h) * g.H + (r0 % tiles_h) * TH) * g.W + tw * TW;
-            __syncthreads();
-        }
 #pragma unroll 1
         for (int k = 0; k < ((SW_KO & 2) ? 0 : 4); ++k) {  // (not unrolled: 9 taps in flight, not 36)
             const int p = (tid >> 4) + 32 * k, pr = p >> 4, pc = p & 15;
-            float4 dq;
-            if constexpr (FUSED) {
-                dq = *reinterpret_cast<const float4*>(&DY[p * CI + 4 * cq]);
-                st4(g.dy_out + (tbase + (int64_t)pr * g.W + pc) * Cin + ci, dq);
-            } else {
-                dq = rdy[0];  // static register indexing: rotate the dy quads
-                rdy[0] = rdy[1];
-                rdy[1] = rdy[2];
-                rdy[2] = rdy[3];
-            }
+            const float4 dq = rdy[0];  // static register indexing: rotate the dy quads
+            rdy[0] = rdy[1];
+            rdy[1] = rdy[2];
+            rdy[2] = rdy[3];
             float4 y = f4(0.f);
 #pragma unroll
             for (int dy_ = 0; dy_ < 3; ++dy_)
 #pragma unroll
                 for (int dx_ = 0; dx_ < 3; ++dx_) {
                     const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
-                    if constexpr (FUSED)
-                        y = fma4(xv, *reinterpret_cast<const float4*>(&KS9[(dy_ * 3 + dx_) * CI + 4 * cq]), y);
-                    else
-                        y = fma4(xv, kt[dy_ * 3 + dx_], y);
+                    y = fma4(xv, kt[dy_ * 3 + dx_], y);
                     dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
                 }
             *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
         }
-        if constexpr (!(SW_KO & 4) && !FUSED) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
+        if constexpr (!(SW_KO & 4)) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
         __syncthreads();
 #pragma unroll 4
         for (int s = 0; s < ((SW_KO & 1) ? 0 : KS); ++s) {
@@ -325,6 +250,223 @@ __global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
     if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 32 * 16 + (tid % 16)]);
 }
 
+// ------------------------------------------------------------------------------------------
+// The fused block backward (unet_sepconv_bwd_fused): the whole backward of a 64-output conv block
+// but its depthwise data gradient.  Per 4 x 16 pixel tile: dz formed from (da, z) into LDS, dy =
+// dz . pk^T by MFMA (written out; dz never goes to HBM), y recomputed from the view's halo (the
+// forward's fmaf chain) with the depthwise filter gradient from the same taps, then y^T dz by
+// MFMA.  4-wave blocks, TWO per CU (77.5 KB of LDS each: the dy tile and the y tile share one
+// buffer -- each thread reads its dy quad and writes its y quad at the same place).  The two resident blocks run their barrier-separated phases (staging, dy GEMM,
+// depthwise, weight-gradient GEMM) independently, so one block's MFMAs overlap the other's
+// loads, stores and VALU work; with one 8-wave block per CU every phase ran alone (lab knock-outs,
+// tools/lab/sw_fused_lab.hip: each of the four phases cost 10-30 % of the kernel additively;
+// this form: enc1_block2 320 -> 307 us, dec1_block1 597 -> 532 us, step +1.2 %).
+// A block walks its run of tiles down a column (th fastest): consecutive tiles share two halo rows.
+namespace fb {
+constexpr int TH = 4, TW = 16, HWp = TW + 2, HPIX = (TH + 2) * HWp;  // 108 halo pixels
+constexpr int PX = TH * TW;                                          // 64 pixels per tile
+constexpr int NT = 256, CI = 64, CO = 64, ZS = CO + 1;
+constexpr int NHQ = HPIX * (CI / 4);    // halo float4 (1728)
+constexpr int HR = (NHQ + NT - 1) / NT;  // per thread (7)
+constexpr int DQ = PX * (CO / 4) / NT;   // dz float4 per thread (4)
+constexpr int L_X = HPIX * CI, L_YD = PX * CI, L_Z = PX * ZS, L_W = CO * CI, L_K = 9 * CI;
+constexpr int SIZE = L_X + L_YD + L_Z + L_W + L_K;  // 19840 floats (77.5 KB)
+static_assert(CI * CO <= SIZE && 9 * 16 * 16 * 4 <= SIZE, "epilogue scratch");
+static_assert(2 * SIZE * 4 <= 160 * 1024, "two blocks per CU");
+}  // namespace fb
+
+template <int MODE>
+__global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) {
+    constexpr int TH = fb::TH, TW = fb::TW, HWp = fb::HWp, PX = fb::PX, NT = fb::NT, CI = fb::CI, CO = fb::CO;
+    constexpr int ZS = fb::ZS, NHQ = fb::NHQ, HR = fb::HR, DQ = fb::DQ;
+    __shared__ __attribute__((aligned(16))) float smem[fb::SIZE];
+    float* Xs = smem;
+    float* YD = Xs + fb::L_X;  // dy tile [px][ci], then (in place) the y tile
+    float* Zs = YD + fb::L_YD;
+    float* Wt = Zs + fb::L_Z;  // [co][ci]
+    float* KS9 = Wt + fb::L_W;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int j = blockIdx.x >> 3;  // XCD-aware (ci group, m-slice) map, as sepconv_wgrad_kernel
+    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
+    const int c0 = CI * cig;
+    const int t_begin = slice * g.tps;
+    const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
+    const int tiles_h = g.H / TH;
+    const int Cin = g.Cin;
+    const int cq = tid & 15, ci = c0 + 4 * cq;
+
+    for (int e = tid; e < 9 * CI; e += NT) KS9[e] = g.dk[(e / CI) * Cin + c0 + e % CI];
+    for (int e = tid; e < CO * CI; e += NT) {  // Wt[co][ci] = pk[c0 + ci][co]
+        const int co = e / CI, cl = e - co * CI;
+        Wt[co * CI + cl] = g.pk[(int64_t)(c0 + cl) * CO + co];
+    }
+    const float* src = g.x.src0;
+    int cs = g.x.c0, cc = ci;
+    const float* scp = g.x.sc0;
+    const float* shp = g.x.sh0;
+    bool bn = MODE == UNET_VIEW_BNRELU;
+    if constexpr (MODE == UNET_VIEW_CONCAT) {
+        if (cc >= g.x.c0) {
+            src = g.x.src1;
+            cs = g.x.c1;
+            cc -= g.x.c0;
+            scp = g.x.sc1;
+            shp = g.x.sh1;
+            bn = true;
+        }
+    }
+    float4 hsc = f4(1.f), hsh = f4(0.f);
+    if constexpr (MODE != UNET_VIEW_PLAIN) {
+        if (bn) {
+            hsc = ld4(scp + cc);
+            hsh = ld4(shp + cc);
+        }
+    }
+    // tile T: column-major walk (th fastest)
+    auto tile_base = [&](int T, int& n, int& h0, int& w0) {
+        const int th = T % tiles_h, r = T / tiles_h, tiles_w = g.W / TW;
+        w0 = (r % tiles_w) * TW;
+        n = r / tiles_w;
+        h0 = th * TH;
+    };
+    float4 hx[HR], rz[DQ], rzz[DQ];
+    bool hok[HR];
+    auto load = [&](int T) {
+        int n, h0, w0;
+        tile_base(T, n, h0, w0);
+#pragma unroll
+        for (int k = 0; k < HR; ++k) {
+            const int e = tid + NT * k;
+            const int pix = e >> 4, r = pix / HWp, c = pix - r * HWp;
+            const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+            hok[k] = e < NHQ && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+            hx[k] = ld4(src + ((int64_t)(hok[k] ? (n * g.H + hh) * g.W + ww : 0) * cs + cc));
+        }
+        const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
+#pragma unroll
+        for (int k = 0; k < DQ; ++k) {  // pixel (tid >> 4) + 16 k, output-channel quad cq
+            const int p = (tid >> 4) + 16 * k;
+            const int64_t o = (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * cq;
+            rz[k] = ld4(g.da + o);
+            rzz[k] = ld4(g.z + o);
+        }
+    };
+    auto store = [&]() {
+        // dz = sc (g - p - (z - mu) q), g = da [z sc + sh > 0] (as gemm.hip A_BNBWD); this thread's
+        // output-channel quad is cq in every k (BN constants re-read: L1 hits)
+        const float4 fsc = ld4(g.bsc + 4 * cq), fsh = ld4(g.bsh + 4 * cq);
+        const float4 fmu = ld4(g.coef + 4 * cq), fp = ld4(g.coef + CO + 4 * cq), fq = ld4(g.coef + 2 * CO + 4 * cq);
+#pragma unroll
+        for (int k = 0; k < HR; ++k) {
+            const int e = tid + NT * k;
+            float4 v = hx[k];
+            if constexpr (MODE != UNET_VIEW_PLAIN) {
+                if (bn) v = bnrelu4(v, hsc, hsh);
+            }
+            if (!hok[k]) v = f4(0.f);
+            if (e < NHQ) *reinterpret_cast<float4*>(&Xs[(e >> 4) * CI + 4 * (e & 15)]) = v;
+        }
+#pragma unroll
+        for (int k = 0; k < DQ; ++k) {
+            float4 v = rz[k];
+            const float4 zz = rzz[k];
+            v.x = fmaf(zz.x, fsc.x, fsh.x) > 0.f ? v.x : 0.f;
+            v.y = fmaf(zz.y, fsc.y, fsh.y) > 0.f ? v.y : 0.f;
+            v.z = fmaf(zz.z, fsc.z, fsh.z) > 0.f ? v.z : 0.f;
+            v.w = fmaf(zz.w, fsc.w, fsh.w) > 0.f ? v.w : 0.f;
+            v.x = fsc.x * (v.x - fp.x - (zz.x - fmu.x) * fq.x);
+            v.y = fsc.y * (v.y - fp.y - (zz.y - fmu.y) * fq.y);
+            v.z = fsc.z * (v.z - fp.z - (zz.z - fmu.z) * fq.z);
+            v.w = fsc.w * (v.w - fp.w - (zz.w - fmu.w) * fq.w);
+            float* d = &Zs[((tid >> 4) + 16 * k) * ZS + 4 * cq];
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    };
+
+    // dy GEMM: wave w -> pixels 32 (w >> 1) .., channels 32 (w & 1) ..; weight-gradient GEMM:
+    // wave w -> the (32 ci x 32 co) quarter ci 32 (w & 1) .., co 32 (w >> 1) .. over all 64 pixels
+    const int px0 = 32 * (wave >> 1), cl0 = 32 * (wave & 1);
+    const int wci = 32 * (wave & 1), wco = 32 * (wave >> 1);
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    float4 dwa[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) dwa[t] = f4(0.f);
+
+    if (t_begin < t_end) load(t_begin);
+    for (int T = t_begin; T < t_end; ++T) {
+        if constexpr (!(SW_KO & 8)) store();
+        __syncthreads();
+        int n, h0, w0;
+        tile_base(T, n, h0, w0);
+        const int64_t tbase = (int64_t)(n * g.H + h0) * g.W + w0;
+        if constexpr (!(SW_KO & 4)) load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
+        {
+            floatx16 ad;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ad[r] = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < ((SW_KO & 16) ? 0 : CO); k += 2)
+                ad = __builtin_amdgcn_mfma_f32_32x32x2f32(Zs[(px0 + lo) * ZS + k + hi], Wt[(k + hi) * CI + cl0 + lo], ad,
+                                                          0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) YD[(px0 + acc_row(r, hi)) * CI + cl0 + lo] = ad[r];
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int k = 0; k < ((SW_KO & 2) ? 0 : 4); ++k) {  // (not unrolled: 9 taps in flight, not 36)
+            const int p = (tid >> 4) + 16 * k, pr = p >> 4, pc = p & 15;
+            float4* yd = reinterpret_cast<float4*>(&YD[p * CI + 4 * cq]);
+            const float4 dq = *yd;
+            if constexpr (!(SW_KO & 32)) st4(g.dy_out + (tbase + (int64_t)pr * g.W + pc) * Cin + ci, dq);
+            float4 y = f4(0.f);
+#pragma unroll
+            for (int dy_ = 0; dy_ < 3; ++dy_)
+#pragma unroll
+                for (int dx_ = 0; dx_ < 3; ++dx_) {
+                    const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
+                    y = fma4(xv, *reinterpret_cast<const float4*>(&KS9[(dy_ * 3 + dx_) * CI + 4 * cq]), y);
+                    dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
+                }
+            *yd = y;  // the same thread read this slot's dy above
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int s = 0; s < ((SW_KO & 1) ? 0 : PX / 2); ++s) {
+            const int p = 2 * s + hi;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(YD[p * CI + wci + lo], Zs[p * ZS + wco + lo], acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+    float* E = smem;  // pointwise slab rows c0 .. c0+63: [64 ci][CO]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) E[(wci + acc_row(r, hi)) * CO + wco + lo] = acc[r];
+    __syncthreads();
+    float* pw = g.pw_slab + ((int64_t)slice * Cin + c0) * CO;
+    for (int e = tid; e < CI * CO / 4; e += NT) st4(pw + 4 * e, *reinterpret_cast<const float4*>(&E[4 * e]));
+    __syncthreads();
+    // depthwise slab [t][ci]: the 16 threads of each channel quad, fixed-order tree
+    float4* D = reinterpret_cast<float4*>(smem);  // [9][16 pixel rows][16 quads]
+#pragma unroll
+    for (int t = 0; t < 9; ++t) D[(t * 16 + (tid >> 4)) * 16 + cq] = dwa[t];
+    __syncthreads();
+    for (int o = 8; o > 0; o >>= 1) {
+        for (int e = tid; e < 9 * o * 16; e += NT) {
+            const int t = e / (o * 16), rr = (e / 16) % o, q = e % 16;
+            D[(t * 16 + rr) * 16 + q] = add4(D[(t * 16 + rr) * 16 + q], D[(t * 16 + rr + o) * 16 + q]);
+        }
+        __syncthreads();
+    }
+    float* dws = g.dw_slab + (int64_t)slice * 9 * Cin;
+    if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 16 * 16 + (tid % 16)]);
+}
+
 int resident_cus() {
     static int cus = 0;
     if (!cus) {
@@ -339,13 +481,14 @@ int resident_cus() {
 struct SwPlan {
     int tiles, ncig, S, tps;
 };
-SwPlan sw_plan(int n, int h, int w, int cin) {
+SwPlan sw_plan(int n, int h, int w, int cin, bool fused = false) {
     SwPlan p;
-    p.tiles = n * (h / TH) * (w / TW);
+    p.tiles = fused ? n * (h / fb::TH) * (w / fb::TW) : n * (h / TH) * (w / TW);
     p.ncig = cin / CI;
-    // one block per CU (110-142 KB of LDS): m-slices a multiple of 8 (the XCD map).  (128 / 192
-    // blocks, leaving CUs to the main stream, measured -1.7 / -0.3 % img/s.)
-    int S = (int)cdiv(resident_cus(), p.ncig);
+    // filter-only kernel: one block per CU (110-142 KB of LDS); fused block backward: two per CU.
+    // m-slices a multiple of 8 (the XCD map).  (128 / 192 blocks, leaving CUs to the main stream,
+    // measured -1.7 / -0.3 % img/s.)
+    int S = (int)cdiv((fused ? 2 : 1) * resident_cus(), p.ncig);
     S = (int)cdiv(S, 8) * 8;
     p.tps = (int)cdiv(p.tiles, S);
     p.S = S;
@@ -354,7 +497,7 @@ SwPlan sw_plan(int n, int h, int w, int cin) {
 
 template <int MODE, bool DROP>
 void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
-    if (a.da) sepconv_wgrad_kernel<MODE, false, 64, true><<<blocks, NT, 0, st>>>(a);
+    if (a.da) sepconv_bwd_fused_kernel<MODE><<<blocks, fb::NT, 0, st>>>(a);
     else if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
     else sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
 }
@@ -380,7 +523,8 @@ extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int 
 extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout) {
     if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || (cout != 64 && cout != 128) || h % TH || w % TW)
         return 0;
-    const SwPlan p = sw_plan(n, h, w, cin);
+    // the larger of the two plans (the fused block backward, 64 outputs, runs twice the slices)
+    const SwPlan p = sw_plan(n, h, w, cin, cout == 64);
     return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
 }
 
@@ -390,7 +534,7 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
     const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w, cin);
+    const SwPlan p = sw_plan(n, h, w, cin, a.da != nullptr);
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;
