@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 9
+#define UNET_ABI_VERSION 10
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -215,9 +215,14 @@ int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float
  * from unet_bn_relu_bwd_stats(_finish) (exactly unet_pointwise_bwd_data_bnrelu's dz), then
  * dy = dz . pw_kernel^T (written out, for the depthwise data gradient), d_pw_kernel = y^T dz and
  * d_dw_kernel as above; dz never goes to memory (bytes: da, z, the input view, dy).  No dropout
- * on either side.  Workspace as unet_sepconv_bwd_filter.                                      */
+ * on either side.  Workspace as unet_sepconv_bwd_filter.
+ * da may be NULL when da_dlogit (m floats) and da_kernel (cout floats) are given: the binary
+ * head's gradient is rank one, da[m][c] = da_dlogit[m] * da_kernel[c] (unet_head_bwd_bnstats'
+ * dlogit output and the head's 1x1 kernel, model/u_net.py:105-112), formed on load with the
+ * same product the head would have stored (ABI 10).                                          */
 int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                           const float* pw_kernel, const float* da, const float* z,
+                           const float* pw_kernel, const float* da, const float* da_dlogit,
+                           const float* da_kernel, const float* z,
                            const float* scale, const float* shift, const float* coef, int cout,
                            float* dy, float* d_dw_kernel, float* d_pw_kernel, void* ws,
                            size_t ws_bytes, unet_stream_t stream);
@@ -377,13 +382,16 @@ int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
                   void* ws, size_t ws_bytes, unet_stream_t stream);
 /* Binary head on a BNRELU view: unet_head_bwd plus the BatchNorm-backward
  * partial sums of the head input's block (dx is all of its da; bn_partials
- * layout and finish as unet_dwconv3x3_bwd_data_bnstats).  _slabs: S, or 0. */
+ * layout and finish as unet_dwconv3x3_bwd_data_bnstats).  _slabs: S, or 0.
+ * dx may be NULL when dlogit (m floats) is given: dx = dlogit (x) kernel is
+ * rank one, so only dL/dlogit per pixel is stored and the consumer forms dx
+ * on load (unet_sepconv_bwd_fused's da_dlogit; ABI 10).                     */
 int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls);
 int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls,
                           const float* kernel, const float* prob,
                           const float* y_true, const float* sums, float smooth,
                           int loss_kind, float loss_scale, float* dx,
-                          float* dkernel, float* dbias,
+                          float* dlogit, float* dkernel, float* dbias,
                           const float* mean, const float* rstd,
                           float* bn_partials, void* ws, size_t ws_bytes,
                           unet_stream_t stream);

@@ -714,6 +714,17 @@ def test_head_bwd_bnstats(ops, use_bn, loss_kind):
         outs.append((dx, dk, db))
     for x, y in zip(outs[0], outs[1]):
         assert torch.equal(x, y)
+    # rank-one form (ABI 10): only dL/dlogit per pixel goes out; dx == dlogit (x) kernel bitwise,
+    # the same weight / bias gradients and BN-backward partials
+    dl, dk1, db1 = torch.empty(n * h * w, device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
+    part1 = torch.zeros_like(part)
+    ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1,
+                         mean if use_bn else None, rstd if use_bn else None, part1, dlogit=dl)
+    assert torch.equal(dl[:, None] * k.reshape(1, c), outs[0][0].reshape(-1, c))
+    assert torch.equal(dk1, outs[0][1]) and torch.equal(db1, outs[0][2])
+    assert torch.equal(part1, part)
+    with pytest.raises(ValueError):  # neither dx nor dlogit
+        ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1, None, None, part1)
     m = n * h * w
     st = []
     for fused in (True, False):
@@ -865,6 +876,21 @@ def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn):
     assert rel_err(host(dy_f).reshape(m, C), host(dy_r)) < 2e-6
     assert rel_err(host(dpk_f), host(dpk_r)) < 2e-6
     assert rel_err(host(ddk_f), host(ddk_r)) < 2e-6
+    # the binary head's rank-one da (ABI 10): da = dlogit (x) kernel formed on load, bitwise the same
+    dlg = dev(f32(rng.standard_normal(m)))
+    hk = dev(f32(rng.standard_normal(cout) * 0.3))
+    da1 = dlg[:, None] * hk[None, :]
+    outs1 = []
+    for r1 in (False, True):
+        dy1 = torch.full((n, h, w, C), 7.0, device="cuda")
+        ddk1, dpk1 = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
+        if r1:
+            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, None, tz, ts, th, coef, cout, dy1, ddk1, dpk1, da_rank1=(dlg, hk))
+        else:
+            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, da1, tz, ts, th, coef, cout, dy1, ddk1, dpk1)
+        outs1.append((dy1, ddk1, dpk1))
+    for x1, x2 in zip(*outs1):
+        assert torch.equal(x1, x2)
     # float64 oracle
     if use_bn:
         rz, _, _ = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var))

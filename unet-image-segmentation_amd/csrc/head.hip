@@ -261,7 +261,9 @@ __device__ __forceinline__ float loss_grad(float t, const float* s3, float smoot
 // STATS (BNRELU view): dx is the whole da of the last decoder block, so the kernel also emits
 // that block's BatchNorm-backward partial sums (bnpart[block][0][c] = sum g, [1][c] = sum g*xhat,
 // g = dx*[z*sc+sh > 0], xhat = (z-mu)*rs) instead of leaving them to a pass over (dx, z).
-template <int MODE, int LOSS, bool STATS = false>
+// DLOUT (with STATS): dx = dlogit (x) W is rank one; only dlogit goes out (one float per pixel,
+// `dx` is the dlogit buffer) and the consumer forms dx on load with the same product.
+template <int MODE, int LOSS, bool STATS = false, bool DLOUT = false>
 __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int64_t hw, const float* __restrict__ W,
                                                         const float* __restrict__ prob, const float* __restrict__ yt,
                                                         const float* __restrict__ sums, float smooth, float gscale,
@@ -297,6 +299,9 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int6
                 dl = g * p * (1.0f - p);
             }
             dls[threadIdx.x] = dl;
+            if constexpr (DLOUT) {
+                if (m < M) dx[m] = dl;
+            }
             db += dl;
         }
         __syncthreads();
@@ -309,7 +314,7 @@ __global__ __launch_bounds__(256) void head_bwd1_kernel(DView v, int64_t M, int6
                 const float4 a = bnrelu4(zr, hsc, hsh);
                 dw = fma4(a, f4(dl), dw);
                 const float4 d = mul4(w4, f4(dl));
-                st4(dx + m * Cin + 4 * kq, d);
+                if constexpr (!DLOUT) st4(dx + m * Cin + 4 * kq, d);
                 const float4 gm = make_float4(a.x > 0.f ? d.x : 0.f, a.y > 0.f ? d.y : 0.f, a.z > 0.f ? d.z : 0.f,
                                               a.w > 0.f ? d.w : 0.f);
                 s1 = add4(s1, gm);
@@ -590,7 +595,7 @@ int head_bwd_grid(int64_t M) {
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
                   const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
                   float* dkernel, float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs,
-                  float* bnpart, unet_stream_t stream);
+                  float* bnpart, unet_stream_t stream, float* dlogit = nullptr);
 }  // namespace
 
 extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls) {
@@ -601,16 +606,17 @@ extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int
 
 extern "C" int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
                                      const float* prob, const float* y_true, const float* sums, float smooth,
-                                     int loss_kind, float loss_scale, float* dx, float* dkernel, float* dbias,
-                                     const float* mean,
+                                     int loss_kind, float loss_scale, float* dx, float* dlogit, float* dkernel,
+                                     float* dbias, const float* mean,
                                      const float* rstd, float* bn_partials, void* ws, size_t ws_bytes,
                                      unet_stream_t stream) {
     UNET_CHECK_ARG(unet_head_bwd_bnstats_slabs(x, n, h, w, ncls) > 0,
                    "unet_head_bwd_bnstats: needs a binary head on a BNRELU view with Cin %% 4 == 0");
     UNET_CHECK_ARG(bn_partials, "unet_head_bwd_bnstats: null bn_partials");
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_head_bwd_bnstats: mean and rstd go together");
+    UNET_CHECK_ARG((dx == nullptr) != (dlogit == nullptr), "unet_head_bwd_bnstats: give exactly one of dx, dlogit");
     return head_bwd_impl(x, n, h, w, ncls, kernel, prob, y_true, sums, smooth, loss_kind, loss_scale, dx, dkernel,
-                         dbias, ws, ws_bytes, mean, rstd, bn_partials, stream);
+                         dbias, ws, ws_bytes, mean, rstd, bn_partials, stream, dlogit);
 }
 
 extern "C" int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls, const float* kernel,
@@ -625,8 +631,9 @@ namespace {
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
                   const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
                   float* dkernel, float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs,
-                  float* bnpart, unet_stream_t stream) {
+                  float* bnpart, unet_stream_t stream, float* dlogit) {
     if (check_view(x, "unet_head_bwd", true)) return -1;
+    if (dlogit) dx = dlogit;  // (unet_head_bwd_bnstats' rank-one form: the STATS kernel writes dlogit)
     UNET_CHECK_ARG(loss_scale > 0.0f && loss_scale < 1e30f, "unet_head_bwd: loss_scale must be finite and > 0");
     UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
                    "unet_head_bwd: input view must be PLAIN or BNRELU");
@@ -654,7 +661,14 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
 #define UNET_HB1S(L)                                                                                          \
     head_bwd1_kernel<UNET_VIEW_BNRELU, L, true><<<grid, 256, 0, st>>>(v, M, hw, kernel, prob, y_true, sums,   \
                                                                       smooth, gscale, dx, part_w, part_b, mu, rs, bnpart)
-        if (bnpart) {
+#define UNET_HB1D(L)                                                                                          \
+    head_bwd1_kernel<UNET_VIEW_BNRELU, L, true, true><<<grid, 256, 0, st>>>(v, M, hw, kernel, prob, y_true,   \
+                                                                            sums, smooth, gscale, dlogit, part_w, \
+                                                                            part_b, mu, rs, bnpart)
+        if (bnpart && dlogit) {
+            if (loss_kind == UNET_LOSS_DICE) UNET_HB1D(UNET_LOSS_DICE);
+            else UNET_HB1D(UNET_LOSS_IOU);
+        } else if (bnpart) {
             if (loss_kind == UNET_LOSS_DICE) UNET_HB1S(UNET_LOSS_DICE);
             else UNET_HB1S(UNET_LOSS_IOU);
         } else if (x->mode == UNET_VIEW_BNRELU) {
@@ -666,12 +680,13 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
         }
 #undef UNET_HB1
 #undef UNET_HB1S
+#undef UNET_HB1D
         UNET_CHECK_LAUNCH("unet_head_bwd");
         int rc = reduce_slabs(part_w, grid, x->c0, dkernel, x->c0, x->c0, st);
         if (rc) return rc;
         return reduce_slabs(part_b, grid, 1, dbias, 1, 1, st);
     }
-    float* dlogit = static_cast<float*>(ws);
+    float* dlg = static_cast<float*>(ws);
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
     void* ws2 = static_cast<char*>(ws) + dl;
     const size_t ws2_bytes = ws_bytes - dl;
@@ -679,7 +694,7 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
     const int grid = (int)(g > 4096 ? 4096 : g);
 #define UNET_HB(NC, L)                                                                                        \
     head_bwd_kernel<NC, L><<<grid, 256, 0, st>>>(M, hw, x->c0, ncls, kernel, prob, y_true, sums, smooth, gscale, \
-                                                 dlogit, dx)
+                                                 dlg, dx)
     if (ncls == 1) {
         if (loss_kind == UNET_LOSS_DICE) UNET_HB(1, UNET_LOSS_DICE);
         else UNET_HB(1, UNET_LOSS_IOU);
@@ -689,9 +704,9 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
     }
 #undef UNET_HB
     UNET_CHECK_LAUNCH("unet_head_bwd");
-    int rc = head_wgrad(x, M, dlogit, ncls, dkernel, ws2, ws2_bytes, st);
+    int rc = head_wgrad(x, M, dlg, ncls, dkernel, ws2, ws2_bytes, st);
     if (rc) return rc;
-    return colsum(dlogit, M, ncls, dbias, ws2, ws2_bytes, st);
+    return colsum(dlg, M, ncls, dbias, ws2, ws2_bytes, st);
 }
 }  // namespace
 

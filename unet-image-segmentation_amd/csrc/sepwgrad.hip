@@ -65,6 +65,7 @@ struct SwArgs {
     // and raw z exactly as the BN-backward data-gradient GEMM forms it (gemm.hip A_BNBWD), dy =
     // dz . pk^T is computed there and written out (dy_out), and never goes through HBM as dz
     const float *da, *z, *coef, *bsc, *bsh, *pk;
+    const float *da_dl, *da_k;  // rank-one da = da_dl[px] * da_k[c] (the binary head), da NULL
     float* dy_out;
 };
 
@@ -275,7 +276,7 @@ static_assert(CI * CO <= SIZE && 9 * 16 * 16 * 4 <= SIZE, "epilogue scratch");
 static_assert(2 * SIZE * 4 <= 160 * 1024, "two blocks per CU");
 }  // namespace fb
 
-template <int MODE>
+template <int MODE, bool DA1 = false>
 __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) {
     constexpr int TH = fb::TH, TW = fb::TW, HWp = fb::HWp, PX = fb::PX, NT = fb::NT, CI = fb::CI, CO = fb::CO;
     constexpr int ZS = fb::ZS, NHQ = fb::NHQ, HR = fb::HR, DQ = fb::DQ;
@@ -347,8 +348,9 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {  // pixel (tid >> 4) + 16 k, output-channel quad cq
             const int p = (tid >> 4) + 16 * k;
-            const int64_t o = (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * cq;
-            rz[k] = ld4(g.da + o);
+            const int64_t px = mbase + (int64_t)(p >> 4) * g.W + (p & 15), o = px * CO + 4 * cq;
+            if constexpr (DA1) rz[k].x = g.da_dl[px];  // (the 16 lanes of a pixel read one float)
+            else rz[k] = ld4(g.da + o);
             rzz[k] = ld4(g.z + o);
         }
     };
@@ -357,6 +359,8 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
         // output-channel quad is cq in every k (BN constants re-read: L1 hits)
         const float4 fsc = ld4(g.bsc + 4 * cq), fsh = ld4(g.bsh + 4 * cq);
         const float4 fmu = ld4(g.coef + 4 * cq), fp = ld4(g.coef + CO + 4 * cq), fq = ld4(g.coef + 2 * CO + 4 * cq);
+        float4 fk = f4(0.f);
+        if constexpr (DA1) fk = ld4(g.da_k + 4 * cq);
 #pragma unroll
         for (int k = 0; k < HR; ++k) {
             const int e = tid + NT * k;
@@ -370,6 +374,7 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
 #pragma unroll
         for (int k = 0; k < DQ; ++k) {
             float4 v = rz[k];
+            if constexpr (DA1) v = mul4(fk, f4(rz[k].x));  // the product unet_head_bwd would have stored
             const float4 zz = rzz[k];
             v.x = fmaf(zz.x, fsc.x, fsh.x) > 0.f ? v.x : 0.f;
             v.y = fmaf(zz.y, fsc.y, fsh.y) > 0.f ? v.y : 0.f;
@@ -497,7 +502,8 @@ SwPlan sw_plan(int n, int h, int w, int cin, bool fused = false) {
 
 template <int MODE, bool DROP>
 void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
-    if (a.da) sepconv_bwd_fused_kernel<MODE><<<blocks, fb::NT, 0, st>>>(a);
+    if (a.da_dl) sepconv_bwd_fused_kernel<MODE, true><<<blocks, fb::NT, 0, st>>>(a);
+    else if (a.da) sepconv_bwd_fused_kernel<MODE><<<blocks, fb::NT, 0, st>>>(a);
     else if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
     else sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
 }
@@ -534,7 +540,7 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
     const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w, cin, a.da != nullptr);
+    const SwPlan p = sw_plan(n, h, w, cin, a.da || a.da_dl);
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;
@@ -572,7 +578,8 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
 }  // namespace
 
 extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                                      const float* pw_kernel, const float* da, const float* z, const float* scale,
+                                      const float* pw_kernel, const float* da, const float* da_dlogit,
+                                      const float* da_kernel, const float* z, const float* scale,
                                       const float* shift, const float* coef, int cout, float* dy, float* d_dw_kernel,
                                       float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
     const char* op = "unet_sepconv_bwd_fused";
@@ -580,14 +587,18 @@ extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, c
     UNET_CHECK_ARG(cout == 64 && unet_sepconv_bwd_filter_supported(x, n, h, w, cout) && x->drop_rate == 0.f,
                    "%s: unsupported (needs 64 output channels, input channels %% 64 == 0, no dropout on the input, "
                    "a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)", op);
-    UNET_CHECK_ARG(dw_kernel && pw_kernel && da && z && scale && shift && coef && dy && d_dw_kernel && d_pw_kernel,
+    UNET_CHECK_ARG(dw_kernel && pw_kernel && z && scale && shift && coef && dy && d_dw_kernel && d_pw_kernel,
                    "%s: null pointer", op);
-    UNET_CHECK_ARG(((uintptr_t)da | (uintptr_t)z | (uintptr_t)dy | (uintptr_t)scale | (uintptr_t)shift |
+    UNET_CHECK_ARG(da ? !da_dlogit && !da_kernel : da_dlogit && da_kernel,
+                   "%s: give da, or da_dlogit and da_kernel (rank-one da)", op);
+    UNET_CHECK_ARG(((uintptr_t)da | (uintptr_t)da_kernel | (uintptr_t)z | (uintptr_t)dy | (uintptr_t)scale | (uintptr_t)shift |
                     (uintptr_t)coef | (uintptr_t)dw_kernel | (uintptr_t)x->src0 |
                     (uintptr_t)(x->src1 ? x->src1 : x->src0)) % 16 == 0,
                    "%s: operands must be 16-B aligned", op);
     SwArgs a{};
     a.da = da;
+    a.da_dl = da_dlogit;
+    a.da_k = da_kernel;
     a.z = z;
     a.coef = coef;
     a.bsc = scale;

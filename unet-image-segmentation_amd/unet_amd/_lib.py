@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -67,8 +67,8 @@ SIGNATURES = {
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_int, P, P, P, c_size_t, P]),
-    "unet_sepconv_bwd_fused": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, c_int, P, P, P, P, c_size_t,
-                                       P]),
+    "unet_sepconv_bwd_fused": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P,
+                                       c_size_t, P]),
     "unet_sepconv_set_schedule": (c_int, [c_int]),
     "unet_bn_finalize": (c_int, [P, c_int64, c_int, P, P, c_float, c_float, P, P, c_int, P, P, P, P, P]),
     "unet_bn_infer_params": (c_int, [P, P, P, P, c_int, c_float, P, P, P]),
@@ -94,8 +94,8 @@ SIGNATURES = {
     "unet_dice_fwd": (c_int, [P, P, c_int, c_int64, c_int, c_float, P, P, P, c_size_t, P]),
     "unet_head_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_head_bwd_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int, c_int]),
-    "unet_head_bwd_bnstats": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, c_float, P, P, P, P, P, P,
-                                      P, c_size_t, P]),
+    "unet_head_bwd_bnstats": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, c_float, P, P, P, P, P,
+                                      P, P, c_size_t, P]),
     "unet_head_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, c_float, P, P, P, P, c_size_t,
                               P]),
     "unet_meaniou_update": (c_int, [P, P, c_int64, c_int, c_float, P, P]),

@@ -92,6 +92,8 @@ class BlockBufs:
     bnpart_s: int = -1  # the slab count bnpart's counters were last laid out for
     y_recompute: bool = False  # last training forward kept no y: the weight grads recompute it
     zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
+    dlogit: Optional[torch.Tensor] = None  # last block, binary head: dL/dlogit per pixel (its da is rank one)
+    da_rank1: bool = False  # this backward's da is dlogit (x) the head kernel, never materialised
 
 
 @dataclass
@@ -536,8 +538,9 @@ class UNetEngine:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
         dk, pk = self._wts(b, refresh=False)
         img_wg = False
-        fused_bwd = self.fuse_block_bwd and self.fuse_bn_bwd and bb.y_recompute and drop_rate == 0.0 and \
-            b.cout == 64
+        fused_bwd = self._fused_bwd(b, bb, drop_rate)
+        if bb.da_rank1 and not fused_bwd:
+            raise RuntimeError(f"{b.name}: rank-one da without the fused block backward")
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
             if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
@@ -555,8 +558,13 @@ class UNetEngine:
                                                     bb.y, dy, self._gwts(b)[1])
             elif fused_bwd:  # dy and both weight gradients in one pass over (da, z, the input view)
                 gdk_f, gpk_f = self._gwts(b)
-                ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, bb.da, bb.z, bb.scale, bb.shift, bb.coef, b.cout, dy,
-                                      gdk_f, gpk_f)
+                if bb.da_rank1:  # the binary head's da = dlogit (x) kernel, formed on load
+                    ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, None, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
+                                          dy, gdk_f, gpk_f, da_rank1=(bb.dlogit, self.vars["output_mask/kernel"]))
+                    bb.da_rank1 = False
+                else:
+                    ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, bb.da, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
+                                          dy, gdk_f, gpk_f)
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, dz)
@@ -607,6 +615,10 @@ class UNetEngine:
                 ops.dwconv3x3_bwd_data(view_in, n, h, w, dk, dy, dx0, dx1)
         self._grads_ready(f"{b.name}_sepconv/depthwise_kernel")
 
+    def _fused_bwd(self, b: Block, bb: BlockBufs, drop_rate: float = 0.0) -> bool:
+        """The block's backward runs as one unet_sepconv_bwd_fused pass."""
+        return self.fuse_block_bwd and self.fuse_bn_bwd and bb.y_recompute and drop_rate == 0.0 and b.cout == 64
+
     def _view_of(self, A: Acts, b: Block) -> View:
         bb = A.blocks[b.name]
         return View.bnrelu(bb.z, bb.scale, bb.shift)
@@ -622,11 +634,18 @@ class UNetEngine:
         S = (ops.head_bwd_bnstats_slabs(hv, n, self.h, self.w, self.num_classes)
              if self.fuse_bn_stats and self.fuse_bn_bwd else 0)
         if S > 0:  # the head's dx is all of the last block's da: emit its BN-backward partials too
+            # binary head feeding the fused block backward: da = dlogit (x) kernel stays rank one
+            # (one float per pixel stored instead of the 64-channel da, formed again on load)
+            rank1 = self._fused_bwd(last, lb)
+            if rank1 and (lb.dlogit is None or lb.dlogit.numel() != n * self.h * self.w):
+                lb.dlogit = torch.empty(n * self.h * self.w, dtype=torch.float32, device=self.device)
             ops.head_bwd_bnstats(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"], A.prob,
-                                 y_true, A.sums, SMOOTH, loss_kind, lb.da, self.gvars["output_mask/kernel"],
-                                 self.gvars["output_mask/bias"], lb.mean if self.use_bn else None,
-                                 lb.rstd if self.use_bn else None, self._bnpart(lb, S, hv.channels), loss_scale)
+                                 y_true, A.sums, SMOOTH, loss_kind, None if rank1 else lb.da,
+                                 self.gvars["output_mask/kernel"], self.gvars["output_mask/bias"],
+                                 lb.mean if self.use_bn else None, lb.rstd if self.use_bn else None,
+                                 self._bnpart(lb, S, hv.channels), loss_scale, dlogit=lb.dlogit if rank1 else None)
             lb.bn_slabs = S
+            lb.da_rank1 = rank1
         else:
             ops.head_bwd(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"],
                          A.prob, y_true, A.sums, SMOOTH, loss_kind, lb.da,

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass, replace
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -401,15 +401,26 @@ def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> 
     return bool(L.load().unet_sepconv_bwd_filter_supported(ctypes.byref(vs), n, h, w, cout))
 
 
-def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, da: Tensor, z: Tensor, scale: Tensor,
-                      shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Tensor, dpk: Tensor):
+def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, da: Optional[Tensor], z: Tensor,
+                      scale: Tensor, shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Tensor, dpk: Tensor,
+                      da_rank1: Optional[Tuple[Tensor, Tensor]] = None):
     """A 64-output block's BN + ReLU backward, pointwise data gradient and both weight gradients
-    in one pass (dz never stored): dy out, d_depthwise / d_pointwise kernels overwritten."""
+    in one pass (dz never stored): dy out, d_depthwise / d_pointwise kernels overwritten.
+    da_rank1 = (dlogit (m,), head kernel (cout,)) instead of da: the binary head's rank-one
+    gradient, formed on load."""
     C = x.channels
     m = n * h * w
     _check(dk, "depthwise_kernel", 9 * C)
     _check(pk, "pointwise_kernel", C * cout)
-    _check(da, "da", m * cout)
+    if (da is None) == (da_rank1 is None):
+        raise ValueError("sepconv_bwd_fused: give da or da_rank1")
+    if da is not None:
+        _check(da, "da", m * cout)
+        da_bytes = 4.0 * m * cout
+    else:
+        _check(da_rank1[0], "da_dlogit", m)
+        _check(da_rank1[1], "da_kernel", cout)
+        da_bytes = 4.0 * m
     _check(z, "z", m * cout)
     _check(coef, "coef", 3 * cout)
     _check(dy, "dy", m * C)
@@ -418,8 +429,9 @@ def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, d
     ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
     vs = x.c_struct()
     _call("unet_sepconv_bwd_fused", (4.0 * m * C * cout + 36.0 * m * C,
-                                     x.src_bytes(n, h, w) + 4.0 * (m * C + 2 * m * cout)),
-          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(pk), _ptr(da), _ptr(z), _ptr(scale), _ptr(shift), _ptr(coef), cout,
+                                     x.src_bytes(n, h, w) + 4.0 * (m * C + m * cout) + da_bytes),
+          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(pk), _ptr(da), _ptr(da_rank1[0] if da_rank1 else None),
+          _ptr(da_rank1[1] if da_rank1 else None), _ptr(z), _ptr(scale), _ptr(shift), _ptr(coef), cout,
           _ptr(dy), _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
 
 
@@ -621,21 +633,28 @@ def head_bwd_bnstats_slabs(x: View, n, h, w, ncls) -> int:
 
 
 def head_bwd_bnstats(x: View, n, h, w, ncls, k: Tensor, prob: Tensor, y_true: Tensor, sums: Tensor, smooth: float,
-                     loss_kind: int, dx: Tensor, dk: Tensor, db: Tensor, mean, rstd, partials: Tensor,
-                     loss_scale: float = 1.0):
-    """head_bwd that also emits the BN-backward partials of the head input's block."""
+                     loss_kind: int, dx: Optional[Tensor], dk: Tensor, db: Tensor, mean, rstd, partials: Tensor,
+                     loss_scale: float = 1.0, dlogit: Optional[Tensor] = None):
+    """head_bwd that also emits the BN-backward partials of the head input's block.  With dlogit
+    (m,) instead of dx, only dL/dlogit per pixel is stored (dx = dlogit (x) kernel, rank one)."""
     S = head_bwd_bnstats_slabs(x, n, h, w, ncls)
     _check(prob, "prob", n * h * w * ncls)
     _check(y_true, "y_true", n * h * w * ncls)
-    _check(dx, "dx", n * h * w * x.c0)
+    if (dx is None) == (dlogit is None):
+        raise ValueError("head_bwd_bnstats: give dx or dlogit")
+    if dx is not None:
+        _check(dx, "dx", n * h * w * x.c0)
+    else:
+        _check(dlogit, "dlogit", n * h * w)
     _check(partials, "bn_partials", bn_stats_partials_numel(S, x.c0))
     ws, wsb = _ws(L.query("unet_head_bwd_workspace", n, h, w, x.c0, ncls), prob.device)
     vs = x.c_struct()
     m = n * h * w
-    _call("unet_head_bwd_bnstats", (4.0 * m * x.c0 * ncls, x.src_bytes(n, h, w) + 4.0 * m * (x.c0 + 2 * ncls)),
+    _call("unet_head_bwd_bnstats", (4.0 * m * x.c0 * ncls,
+                                    x.src_bytes(n, h, w) + 4.0 * m * ((x.c0 if dx is not None else 1) + 2 * ncls)),
           ctypes.byref(vs), n, h, w, ncls, _ptr(k), _ptr(prob), _ptr(y_true), _ptr(sums), float(smooth),
-          int(loss_kind), float(loss_scale), _ptr(dx), _ptr(dk), _ptr(db), _ptr(mean), _ptr(rstd), _ptr(partials), ws,
-          wsb, _stream())
+          int(loss_kind), float(loss_scale), _ptr(dx), _ptr(dlogit), _ptr(dk), _ptr(db), _ptr(mean), _ptr(rstd),
+          _ptr(partials), ws, wsb, _stream())
 
 
 def meaniou_update(y_true: Tensor, y_pred: Tensor, num_classes: int, threshold: Optional[float],
