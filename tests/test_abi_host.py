@@ -29,6 +29,26 @@ def test_library_exports_every_declared_symbol():
     assert lib.unet_abi_version() == _lib.ABI_VERSION
 
 
+def _prototypes():
+    """name -> parameter count of every prototype in the header."""
+    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    out = {}
+    for name, params in re.findall(r"\b(unet_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", txt):
+        params = params.strip()
+        out[name] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_argument_counts_match_header():
+    """Every ctypes argtypes list has exactly as many entries as the C prototype has parameters
+    (a mismatch only surfaces as a ctypes ArgumentError at the first call on the GPU box)."""
+    from unet_amd import _lib
+    protos = _prototypes()
+    assert set(protos) == set(_lib.SIGNATURES)
+    for name, (_, argtypes) in _lib.SIGNATURES.items():
+        assert len(argtypes) == protos[name], (name, len(argtypes), protos[name])
+
+
 def test_view_struct_layout_matches_c():
     from unet_amd._lib import UnetView
     # int32 x4, 6 pointers, float, int32, uint64 -> 16 + 48 + 8 + 8 = 80 bytes, 8-aligned

@@ -7,3 +7,4 @@ run opstests 300 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 -
 run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 run bench 400 python bench.py --no-cpu-baseline --encoder-batch 0
 run bench2 400 python bench.py --no-cpu-baseline --encoder-batch 0
+run host 300 python tools/host_overhead.py

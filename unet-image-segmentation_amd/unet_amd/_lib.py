@@ -95,7 +95,7 @@ SIGNATURES = {
     "unet_head_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_head_bwd_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_head_bwd_bnstats": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, c_float, P, P, P, P, P,
-                                      P, P, c_size_t, P]),
+                                      P, P, P, c_size_t, P]),
     "unet_head_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, c_float, c_int, c_float, P, P, P, P, c_size_t,
                               P]),
     "unet_meaniou_update": (c_int, [P, P, c_int64, c_int, c_float, P, P]),
