@@ -801,9 +801,36 @@ def test_sepconv_pool_selection_epilogue(ops, sep_schedule, mode, n, h, w, c0, c
     assert torch.equal(zsel, ref)
 
 
+@pytest.mark.parametrize("n,h,w,c0,cout", [(2, 8, 16, 64, 64), (1, 16, 32, 128, 128), (1, 8, 16, 128, 256),
+                                           (2, 8, 16, 256, 256), (1, 8, 32, 64, 320)])
+def test_sepconv_pool_selection_epilogue_split_precision(ops, n, h, w, c0, cout):
+    """The split-precision register-A kernel's pool-selection epilogue (64 / 128 / 256-column
+    tiles) equals unet_pool_select of its own z, bitwise."""
+    rng = np.random.default_rng(17 + cout)
+    a, t = _view_inputs(rng, 1, n, h, w, c0, 0)
+    dk = dev(f32(rng.standard_normal((3, 3, c0, 1))))
+    pk = dev(f32(rng.standard_normal((1, 1, c0, cout)) / np.sqrt(c0)))
+    pkx = torch.empty(3 * c0 * cout, dtype=torch.int16, device="cuda")
+    ops.split_x3(pk, [(0, c0, cout, 0)], pkx)
+    v = _mk_view(ops, 1, t)
+    gamma = dev(f32(rng.standard_normal(cout)))
+    z = torch.empty((n, h, w, cout), device="cuda")
+    zsel = torch.full((n, h // 2, w // 2, cout), 7.0, device="cuda")
+    part = torch.zeros(ops.bn_partials_numel(n * h * w, cout), device="cuda")
+    ops.sepconv_fwd(v, n, h, w, dk, cout, pk, None, z, part, zsel, gamma, pkx=pkx)
+    ref = torch.empty_like(zsel)
+    ops.pool_select(z, n, h, w, cout, gamma, ref)
+    assert torch.equal(zsel, ref)
+    zr = K.pointwise(K.depthwise3x3(view_value(1, a["src0"], a["sc0"], a["sh0"], None, None, None, 0.0, 0), host(dk)),
+                     host(pk))
+    assert rel_err(host(z), zr) < 5e-6
+
+
 @pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop", [(1, 2, 8, 16, 64, 0, 64, 0.0), (1, 1, 16, 32, 128, 0, 128, 0.0),
                                                         (3, 1, 16, 16, 64, 64, 64, 0.2), (0, 2, 8, 32, 96, 0, 192, 0.0),
-                                                        (1, 1, 8, 16, 256, 0, 256, 0.0)])
+                                                        (1, 1, 8, 16, 256, 0, 256, 0.0),
+                                                        # 256-column tiles: two of them, a partial one
+                                                        (3, 1, 8, 16, 256, 256, 512, 0.2), (1, 2, 8, 16, 64, 0, 320, 0.0)])
 def test_fused_sepconv_split_precision(ops, mode, n, h, w, c0, c1, cout, drop):
     """The register-A kernel's bf16x6 variant (pw_kernel_x3 from unet_split_x3): z within the fp32
     path's tolerance of the float64 oracle, the depthwise output y bitwise equal to the fp32

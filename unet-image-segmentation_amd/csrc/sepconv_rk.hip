@@ -39,7 +39,7 @@ struct RkLds {
     // X6: B as three bf16 planes [BN][16 k] (32-byte rows; the two 16-byte k chunks of row n are
     // swapped when bit 3 of n is set, so the fragment reads of 16-lane groups are conflict-free)
     static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = X6 ? 3 * BN * BK / 2 : BK * (BN + 4);
-    static constexpr int SLOTS = X6 ? 2 : 3;           // X6: two slots (53 KB: 3 blocks per CU)
+    static constexpr int SLOTS = X6 ? 2 : 3;           // X6: two slots (53 KB: 3 blocks per CU; 79 KB at BN 256: 2)
     static constexpr int RING = SLOTS * (XSZ + KSZ + BSZ);
     static constexpr int EC = X6 && BN > 64 ? 64 : BN;  // accumulator columns per epilogue pass
     static constexpr int TLD = EC + 4;                  // epilogue transpose row stride
@@ -53,7 +53,7 @@ struct RkLds {
 // (common.h split4) and runs mfma_x6 against the pre-split weight planes (SepArgs::pkx) per 32-column
 // tile: 6 x 32 MFMA cycles per stage and tile instead of 8 x 64.
 template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y, bool X6 = false>
-__global__ __launch_bounds__(256, X6 ? 3 : 2) void sepconv_rk_kernel(SepArgs g) {
+__global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kernel(SepArgs g) {
     static_assert(!X6 || MODE != UNET_VIEW_POOL_BNRELU, "X6: no max-pool views");
     constexpr int TN = BN / 32;                 // MFMA tiles per wave (all BN columns)
     constexpr int NH = HPIX * (BK / 4);         // halo float4 per stage (720)
@@ -489,6 +489,11 @@ void launch_rk_x(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
 }
 
 template <int MODE, bool DROP, int BN>
+void launch_rk_x6(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
+    if constexpr (MODE != UNET_VIEW_POOL_BNRELU) launch_rk_x<MODE, DROP, BN, true>(a, stats, write_y, st);
+}
+
+template <int MODE, bool DROP, int BN>
 void launch_rk_t(const SepArgs& a, bool stats, bool write_y, hipStream_t st) {
     if constexpr (MODE != UNET_VIEW_POOL_BNRELU) {
         if (a.pkx && rk_x6_supported(MODE, a.Cin)) {
@@ -513,11 +518,16 @@ bool rk_supported(int mode, int cin, int cout) {
 
 int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st) {
     if (!rk_supported(mode, a.Cin, a.Cout)) return -1;
-    const int bn = a.Cout <= 64 ? 64 : 128;
-#define UNET_RK(M, D)                                                  \
-    do {                                                               \
-        if (bn == 64) launch_rk_t<M, D, 64>(a, stats, write_y, st);    \
-        else launch_rk_t<M, D, 128>(a, stats, write_y, st);            \
+    // split precision with >= 256 outputs: one 256-column tile (two blocks per CU), so the
+    // depthwise and its halo are evaluated once per pixel tile instead of once per 128 columns,
+    // and the 64 x 64 level's 512 pixel tiles fill the 512 block slots in one round
+    const bool x6 = a.pkx && rk_x6_supported(mode, a.Cin);
+    const int bn = a.Cout <= 64 ? 64 : (x6 && a.Cout >= 256 ? 256 : 128);
+#define UNET_RK(M, D)                                                          \
+    do {                                                                       \
+        if (bn == 64) launch_rk_t<M, D, 64>(a, stats, write_y, st);            \
+        else if (bn == 128) launch_rk_t<M, D, 128>(a, stats, write_y, st);     \
+        else launch_rk_x6<M, D, 256>(a, stats, write_y, st);                   \
     } while (0)
     switch (mode) {
         case UNET_VIEW_PLAIN: if (drop) UNET_RK(UNET_VIEW_PLAIN, true); else UNET_RK(UNET_VIEW_PLAIN, false); break;
