@@ -280,6 +280,8 @@ def main():
     ap.add_argument("--no-fused-bwd", action="store_true",
                     help="64-output blocks: data-gradient GEMM + side-stream weight-gradient pass instead of "
                          "the fused block backward (A/B)")
+    ap.add_argument("--fuse", choices=("auto", "always"), default="auto",
+                    help="fused conv forward on the levels >= 64x64 (auto) or on every level (A/B)")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -312,6 +314,7 @@ def main():
         model.enable_data_parallel()
     model.engine.use_x3 = not args.no_x3
     model.engine.fuse_block_bwd = not args.no_fused_bwd
+    model.engine.fuse_sepconv = args.fuse
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
 
     for _ in range(args.warmup):
