@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 11
+#define UNET_ABI_VERSION 10
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -149,13 +149,10 @@ size_t unet_bn_partials_size(int64_t m, int c); /* bytes of bn_partials */
 int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout,
                        const float* pw_kernel, float* z, float* bn_partials,
                        unet_stream_t stream);
-/* dy[m, ci] = sum_co dz[m, co] * k[ci, co].  ws (optional, NULL = none): with at least
- * unet_pointwise_bwd_data_workspace bytes, the small-m GEMMs (the bottleneck level: few row tiles,
- * long k) split k over several blocks and sum the partials in fixed order (ABI 11).  0: never. */
-size_t unet_pointwise_bwd_data_workspace(int64_t m, int cin, int cout);
+/* dy[m, ci] = sum_co dz[m, co] * k[ci, co] */
 int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout,
-                            const float* pw_kernel, float* dy, void* ws,
-                            size_t ws_bytes, unet_stream_t stream);
+                            const float* pw_kernel, float* dy,
+                            unet_stream_t stream);
 size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout);
 /* d_pw_kernel[ci, co] = sum_m y[m, ci] * dz[m, co] (overwrites) */
 int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_t m,
@@ -294,15 +291,12 @@ int unet_bn_relu_bwd_stats_finish(float* partials, int S, int64_t m, int c,
  * is also stored (the pointwise weight gradient reads it).  cin, cout % 4 == 0.
  * Replaces the backward of model/u_net.py:20-25 (SeparableConv2D pointwise ->
  * BatchNormalization -> ReLU) for the data path.                                 */
-/* ws (optional, as unet_pointwise_bwd_data's; _workspace 0 = never used): the 1024-channel
- * shapes' plain GEMM splits k where the grid is small (ABI 11).                                */
-size_t unet_pointwise_bwd_data_bnrelu_workspace(int64_t m, int cin, int cout);
 int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m,
                                    int cin, int cout, const float* pw_kernel,
                                    const float* scale, const float* shift,
                                    const float* coef, float drop_rate,
                                    uint64_t drop_seed, float* dy, float* dz,
-                                   void* ws, size_t ws_bytes, unet_stream_t stream);
+                                   unet_stream_t stream);
 
 /* The image block (enc1_block1 over the 3-channel input zero-padded to 4):
  * unet_pointwise_bwd_data_bnrelu without dropout, cin == 4, cout 32 or 64,

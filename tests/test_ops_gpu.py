@@ -289,63 +289,6 @@ def test_pointwise_bwd_data_bnrelu(ops, use_bn, drop, m, cin, cout):
 
 
 
-@pytest.mark.parametrize("route", ["pointwise", "bnrelu_dz", "convT"])
-def test_split_k_gemms(ops, route):
-    """The bottleneck level's data-gradient GEMMs (M = 4096 rows: 128-256 tiles, 1024-2048-deep k)
-    split k over several blocks and sum the partials in fixed order (ABI 11): against float64, and
-    deterministic run to run."""
-    L = ops.L
-    rng = np.random.default_rng({"pointwise": 1, "bnrelu_dz": 2, "convT": 3}[route])
-    m = 4096
-    if route == "pointwise":
-        cin, cout = 512, 1024
-        assert L.query("unet_pointwise_bwd_data_workspace", m, cin, cout) > 0  # the split path is taken
-        dz = f32(rng.standard_normal((m, cout)))
-        pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cout))
-        outs = []
-        for _ in range(2):
-            dy = torch.empty((m, cin), device="cuda")
-            ops.pointwise_bwd_data(dev(dz), m, cin, cout, dev(pk), dy)
-            outs.append(dy)
-        ref = dz.astype(np.float64) @ pk[0, 0].T.astype(np.float64)
-    elif route == "bnrelu_dz":
-        cin = cout = 1024
-        assert L.query("unet_pointwise_bwd_data_bnrelu_workspace", m, cin, cout) > 0
-        z = f32(rng.standard_normal((m, 1, 1, cout)) * 2 + 0.3)
-        da = f32(rng.standard_normal((m, 1, 1, cout)))
-        pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cout))
-        gamma, beta = bn_affine(rng, cout)
-        _, mean, var = K.bn_train(z, gamma, beta)
-        rstd = 1 / np.sqrt(var + 1e-3)
-        ts, th = dev(f32(gamma * rstd)), dev(f32(beta - mean * gamma * rstd))
-        coef = torch.empty(3 * cout, device="cuda")
-        ops.bn_relu_bwd_stats(dev(da), dev(z), m, cout, dev(f32(mean)), dev(f32(rstd)), ts, th, True, 0.0, 0,
-                              torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda"), coef)
-        outs = []
-        for _ in range(2):
-            dy = torch.empty((m, cin), device="cuda")
-            dz = torch.empty((m, cout), device="cuda")
-            ops.pointwise_bwd_data_bnrelu(dev(da), dev(z), m, cin, cout, dev(pk), ts, th, coef, 0.0, 0, dy, dz)
-            outs.append(dy)
-        rz, _, _ = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var))
-        ref = rz.reshape(m, cout).astype(np.float64) @ pk[0, 0].T.astype(np.float64)
-    else:
-        n, h, w, cin, cout = 16, 16, 16, 1024, 512
-        x = dev(f32(rng.standard_normal((n, h, w, cin))))
-        v = ops.View.plain(x)
-        k = f32(rng.standard_normal((2, 2, cout, cin)) / np.sqrt(4 * cout))
-        dout = f32(rng.standard_normal((n, 2 * h, 2 * w, cout)))
-        outs = []
-        for _ in range(2):
-            dx = torch.empty((n, h, w, cin), device="cuda")
-            ops.conv_transpose2x2_bwd(v, n, h, w, cout, dev(k), dev(dout), dx, None, None)
-            outs.append(dx)
-        d6 = dout.astype(np.float64).reshape(n, h, 2, w, 2, cout)
-        ref = np.einsum("niajbd,abdc->nijc", d6, k.astype(np.float64)).reshape(m, cin)
-    assert torch.equal(outs[0], outs[1])
-    assert rel_err(host(outs[0]).reshape(m, -1), ref) < 2e-6
-
-
 @pytest.mark.parametrize("mode,drop", [(1, 0.0), (1, 0.2), (0, 0.0)])
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 4, 4, 64, 32), (2, 3, 5, 32, 16), (1, 8, 8, 128, 64)])
 def test_conv_transpose(ops, mode, drop, n, h, w, cin, cout):

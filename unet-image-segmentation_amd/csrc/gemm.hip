@@ -58,10 +58,6 @@ struct RowsArgs {
     float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
     const float *bsc, *bsh, *bmu, *brs;  // E_BNPART: per-column BN scale/shift, mean/rstd (NULL: no xhat)
     float* bnpart;                       // E_BNPART: [cdiv(M, 128)][2][N] partial sums
-    // split K (E_STORE, vectorised kernel): block z sums k in [z kchunk, (z+1) kchunk) into slab z
-    // of kslab ([gridDim.z][M][N]); a fixed-order reduce_slabs writes C.  kchunk 0: no split
-    int kchunk;
-    float* kslab;
 };
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
@@ -473,9 +469,6 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     const int n0 = blockIdx.y * BN;
     const int M_rem = (g.M - m0) < BM ? (int)(g.M - m0) : BM;
     const int K = g.K;
-    // this block's k range (split K: chunk blockIdx.z); K itself stays the channel stride of coef
-    const int kbeg = g.kchunk ? (int)blockIdx.z * g.kchunk : 0;
-    const int kend = g.kchunk && kbeg + g.kchunk < K ? kbeg + g.kchunk : K;
 
     // A: this thread stages k-quad kq of rows arow + (256/KQ) r
     const int kq = tid % KQ;
@@ -523,7 +516,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     auto load_stage = [&](int k0) {
         const int k = k0 + 4 * kq;
         ak = k;
-        const int kc = k < kend ? k : 0;
+        const int kc = k < K ? k : 0;
         int koff = kc;
         if constexpr (AMODE == A_UNSHUFFLE) {
             const int ab = kc / g.uf;
@@ -548,12 +541,12 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const int kk = BKC ? k0 + 4 * bq_k : k0 + bq_k + (256 / NQ) * r;
-            bok[r] = boff[r] >= 0 && kk < kend;
+            bok[r] = boff[r] >= 0 && kk < K;
             rb[r] = ld4(g.B + (bok[r] ? boff[r] + (BKC ? k0 : k0 * sbk) : 0));
         }
     };
     auto store_stage = [&](int buf) {
-        const bool kv = ak < kend;
+        const bool kv = ak < K;
 #pragma unroll
         for (int r = 0; r < AQ; ++r) {
             float4 v = ra[r];
@@ -626,13 +619,13 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
-    const int nk = (kend - kbeg + BK - 1) / BK;
-    load_stage(kbeg);
+    const int nk = (K + BK - 1) / BK;
+    load_stage(0);
     store_stage(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) load_stage(kbeg + (kt + 1) * BK);
+        if (kt + 1 < nk) load_stage((kt + 1) * BK);
         if constexpr (X6) {
 #pragma unroll
             for (int ks = 0; ks < BK / 16; ++ks) {
@@ -687,9 +680,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 
     const bool full = M_rem == BM;  // every row of the tile exists: no per-row checks
     if constexpr (EPI == E_STORE || EPI == E_STATS || EPI == E_BNPART) {
-        // (split K, E_STORE only: this chunk's partial into its slab, dense rows of N)
-        float* const Cb = EPI == E_STORE && g.kchunk ? g.kslab + (int64_t)blockIdx.z * g.M * g.N : g.C;
-        const int ldc = EPI == E_STORE && g.kchunk ? g.N : (int)g.ldc;
+        const int ldc = (int)g.ldc;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -697,7 +688,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                 const int n = n0 + wn * (BN / 2) + tn * 32 + lo;
                 if (n >= g.N) continue;
                 const int rb0 = wm * (BM / 2) + tm * 32 + 4 * hi;  // acc_row(r, hi) = rb0 + acc_row(r, 0)
-                float* cp = Cb + (int64_t)(m0 + rb0) * ldc + n;
+                float* cp = g.C + (int64_t)(m0 + rb0) * g.ldc + n;
                 if (full) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) cp[acc_row(r, 0) * ldc] = acc[tm][tn][r];
@@ -1233,35 +1224,9 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
-// Split K for the small-M plain-epilogue GEMMs (the bottleneck level: M = 4096 rows, 128-256 tiles
-// for 256 CUs, 32-128 k-steps each, one 4-wave block per CU): ks chunks of >= 8 k-steps so that
-// ~1024 blocks run, partials reduced in fixed order.  ks 1: no split.
-int rows_ksplit(int64_t M, int K, int N, const RowsCfg& c) {
-    if (!lab_knob("UNET_SPLITK", 1)) return 1;  // (lab A/B switch; the product library always splits)
-    const int64_t blocks = cdiv(M, 128) * cdiv(N, c.bn);
-    const int nk = (int)cdiv(K, c.bk);
-    if (blocks >= 384 || nk < 16) return 1;
-    int ks = (int)cdiv(1024, blocks);
-    if (ks > nk / 8) ks = nk / 8;
-    if (ks < 2) return 1;
-    const int kchunk = (int)cdiv(cdiv(K, ks), c.bk) * c.bk;
-    return (int)cdiv(K, kchunk);
-}
-
-// bytes of the split-K partial slabs a plain-epilogue GEMM (M x K) . (K x N) needs (0: no split)
-size_t rows_splitk_bytes(int64_t M, int K, int N, int amode) {
-    RowsArgs a{};
-    a.M = M;
-    a.K = K;
-    a.N = N;
-    const int ks = rows_ksplit(M, K, N, rows_cfg(a, amode));
-    return ks > 1 ? align_up((size_t)ks * M * N * sizeof(float), 256) : 0;
-}
-
 template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false>
 void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
-    const unsigned gz = a.kchunk ? (unsigned)cdiv(a.K, a.kchunk) : 1u;
-    dim3 grid((unsigned)cdiv(a.M, 128), (unsigned)cdiv(a.N, BN), gz);
+    dim3 grid((unsigned)cdiv(a.M, 128), (unsigned)cdiv(a.N, BN));
     if (a.sbk == 1) gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
     else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
 }
@@ -1272,16 +1237,9 @@ void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
 bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
 
 template <int AMODE, bool DROP, int EPI>
-int launch_rows(const RowsArgs& a_in, hipStream_t st, const char* what) {
-    RowsArgs a = a_in;
-    a.kchunk = 0;
+int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
     if (rows_vec_ok(a, AMODE)) {
         const RowsCfg c = rows_cfg(a, AMODE);
-        int ks = 1;
-        if constexpr (EPI == E_STORE && AMODE != A_BNBWD) {
-            if (a.kslab) ks = rows_ksplit(a.M, a.K, a.N, c);  // (the caller sized kslab by rows_splitk_bytes)
-            if (ks > 1) a.kchunk = (int)cdiv(cdiv(a.K, ks), c.bk) * c.bk;
-        }
 #ifdef UNET_LAB_BUILD  // (not compiled into the product library)
         if (rows_x6()) {
             launch_rows_tile<128, 16, AMODE, DROP, EPI, true>(a, st);
@@ -1295,7 +1253,6 @@ int launch_rows(const RowsArgs& a_in, hipStream_t st, const char* what) {
         else if (c.bn == 256 && c.bk == 16) launch_rows_tile<256, 16, AMODE, DROP, EPI>(a, st);
         else launch_rows_tile<128, 16, AMODE, DROP, EPI>(a, st);
         UNET_CHECK_LAUNCH(what);
-        if (a.kchunk) return reduce_slabs(a.kslab, (int)cdiv(a.K, a.kchunk), a.M * a.N, a.C, a.N, a.ldc, st);
         return 0;
     }
     if constexpr (AMODE == A_BNBWD || EPI == E_BNPART) {  // vectorised kernel only
@@ -1451,20 +1408,12 @@ extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, 
     return launch_rows<A_PLAIN, false, E_STORE>(a, st, "unet_pointwise_fwd");
 }
 
-extern "C" size_t unet_pointwise_bwd_data_workspace(int64_t m, int cin, int cout) {
-    if (m <= 0 || cin <= 0 || cout <= 0) return 0;
-    return rows_splitk_bytes(m, cout, cin, A_PLAIN);
-}
-
 extern "C" int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout, const float* pw_kernel,
-                                       float* dy, void* ws, size_t ws_bytes, unet_stream_t stream) {
+                                       float* dy, unet_stream_t stream) {
     UNET_CHECK_ARG(dz && pw_kernel && dy, "unet_pointwise_bwd_data: null pointer");
     UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_data: bad sizes");
     UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_bwd_data: tensor too large");
-    const size_t need = unet_pointwise_bwd_data_workspace(m, cin, cout);
-    UNET_CHECK_ARG(!ws || ((uintptr_t)ws & 15) == 0, "unet_pointwise_bwd_data: workspace must be 16-B aligned");
     RowsArgs a{};
-    if (ws && need && ws_bytes >= need) a.kslab = static_cast<float*>(ws);  // (too small or NULL: no split)
     a.a = plain_view(dz, cout);
     a.M = m;
     a.K = cout;
@@ -1508,20 +1457,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(const float* __restrict_
 }
 }  // namespace
 
-namespace {
-// the 1024-channel shapes form dz in a streaming pass and run the plain GEMM (see below)
-bool dgrad_dz_route(int cin, int cout) { return cin >= 1024 || cout >= 1024; }
-}  // namespace
-
-extern "C" size_t unet_pointwise_bwd_data_bnrelu_workspace(int64_t m, int cin, int cout) {
-    if (m <= 0 || cin <= 0 || cout <= 0 || !dgrad_dz_route(cin, cout)) return 0;
-    return rows_splitk_bytes(m, cout, cin, A_PLAIN);
-}
-
 extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout,
                                               const float* pw_kernel, const float* scale, const float* shift,
                                               const float* coef, float drop_rate, uint64_t drop_seed, float* dy,
-                                              float* dz, void* ws, size_t ws_bytes, unet_stream_t stream) {
+                                              float* dz, unet_stream_t stream) {
     UNET_CHECK_ARG(da && z && pw_kernel && scale && shift && coef && dy, "unet_pointwise_bwd_data_bnrelu: null pointer");
     UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_data_bnrelu: bad sizes");
     UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_bwd_data_bnrelu: tensor too large");
@@ -1552,7 +1491,7 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
     // load) form dz once in a streaming pass (~6 TB/s) and run the plain GEMM on it: 12-24 us
     // faster per launch (tools/bench_dgrad.py, profiles/r2h_dgrad_split.log); narrower shapes
     // measured equal or slower that way and keep the fused operand load.
-    if (dz && dgrad_dz_route(cin, cout) && cout % 4 == 0 && rows_vec_ok(a, A_BNBWD)) {
+    if (dz && (cin >= 1024 || cout >= 1024) && cout % 4 == 0 && rows_vec_ok(a, A_BNBWD)) {
         const int64_t work = m * (cout / 4);
         const unsigned grid = (unsigned)(work / 256 < 4096 ? cdiv(work, 256) : 4096);
         if (drop_rate > 0.f)
@@ -1571,8 +1510,6 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
         p.N = cin;
         p.C = dy;
         p.ldc = cin;
-        const size_t need = unet_pointwise_bwd_data_bnrelu_workspace(m, cin, cout);
-        if (ws && need && ws_bytes >= need && ((uintptr_t)ws & 15) == 0) p.kslab = static_cast<float*>(ws);
         return launch_rows<A_PLAIN, false, E_STORE>(p, st, "unet_pointwise_bwd_data_bnrelu");
     }
     if (drop_rate > 0.f)
@@ -1690,8 +1627,7 @@ extern "C" size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int 
     const WgradPlan wp = wgrad_plan(M, 4 * cout, cin);
     size_t a = wgrad_workspace(M, 4 * cout, cin) + align_up((size_t)wp.S * 4 * cout * sizeof(float), 256);
     size_t b = colsum_workspace(4 * M, cout);
-    const size_t c = rows_splitk_bytes(M, 4 * cout, cin, A_UNSHUFFLE);  // the data gradient's split-K slabs
-    return a > b ? (a > c ? a : c) : (b > c ? b : c);
+    return a > b ? a : b;
 }
 
 extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
@@ -1724,7 +1660,6 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
         a.N = cin;
         a.C = dx;
         a.ldc = cin;
-        a.kslab = static_cast<float*>(ws);  // (used only where rows_ksplit splits K; ws holds its slabs)
         int rc = launch_rows<A_UNSHUFFLE, false, E_STORE>(a, st, "unet_conv_transpose2x2_bwd(data)");
         if (rc) return rc;
     }

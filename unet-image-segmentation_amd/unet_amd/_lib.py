@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 11
+ABI_VERSION = 10
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -57,8 +57,7 @@ SIGNATURES = {
     "unet_dwconv3x3_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "unet_bn_partials_size": (c_size_t, [c_int64, c_int]),
     "unet_pointwise_fwd": (c_int, [P, c_int64, c_int, c_int, P, P, P, P]),
-    "unet_pointwise_bwd_data_workspace": (c_size_t, [c_int64, c_int, c_int]),
-    "unet_pointwise_bwd_data": (c_int, [P, c_int64, c_int, c_int, P, P, P, c_size_t, P]),
+    "unet_pointwise_bwd_data": (c_int, [P, c_int64, c_int, c_int, P, P, P]),
     "unet_pointwise_bwd_filter_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_filter": (c_int, [P, P, c_int64, c_int, c_int, P, P, c_size_t, P]),
     "unet_sepconv_fwd_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
@@ -80,9 +79,8 @@ SIGNATURES = {
     "unet_bn_relu_bwd_stats_finish": (c_int, [P, c_int, c_int64, c_int, P, P, c_int, P, P, P, P]),
     "unet_bn_relu_bwd_stats": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,
                                        c_size_t, P]),
-    "unet_pointwise_bwd_data_bnrelu_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_data_bnrelu": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, c_float, c_uint64, P, P,
-                                               P, c_size_t, P]),
+                                               P]),
     "unet_pointwise_bwd_data_bnrelu_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_data_bnrelu_wgrad": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, P, P, P, c_size_t,
                                                      P]),

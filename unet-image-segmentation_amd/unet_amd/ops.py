@@ -313,9 +313,8 @@ def pointwise_bwd_data(dz: Tensor, m, cin, cout, pk: Tensor, dy: Tensor):
     _check(dz, "dz", m * cout)
     _check(pk, "pointwise_kernel", cin * cout)
     _check(dy, "dy", m * cin)
-    ws, wsb = _ws(L.query("unet_pointwise_bwd_data_workspace", m, cin, cout), dy.device)
     _call("unet_pointwise_bwd_data", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(dz), m,
-          cin, cout, _ptr(pk), _ptr(dy), ws, wsb, _stream())
+          cin, cout, _ptr(pk), _ptr(dy), _stream())
 
 
 def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
@@ -520,11 +519,10 @@ def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int
     # (measurement label only) the library forms dz in a streaming pass and runs the plain GEMM
     # when either side has >= 1024 channels (gemm.hip, unet_pointwise_bwd_data_bnrelu)
     route = "dz_pass+gemm" if dz is not None and (cin >= 1024 or cout >= 1024) else "gemm_bnbwd"
-    ws, wsb = _ws(L.query("unet_pointwise_bwd_data_bnrelu_workspace", m, cin, cout), dy.device)
     _call("unet_pointwise_bwd_data_bnrelu",
           (2.0 * m * cin * cout, 4.0 * (2 * m * cout + m * cin + cin * cout) + (4.0 * m * cout if dz is not None else 0)),
           _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), float(drop_rate),
-          int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), ws, wsb, _stream(), route=route)
+          int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream(), route=route)
 
 
 def pointwise_bwd_data_bnrelu_wgrad(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
