@@ -282,6 +282,8 @@ def main():
                          "the fused block backward (A/B)")
     ap.add_argument("--fuse", choices=("auto", "always"), default="auto",
                     help="fused conv forward on the levels >= 64x64 (auto) or on every level (A/B)")
+    ap.add_argument("--recompute-y128", action="store_true",
+                    help="128-output blocks too: no y store, weight gradients recompute it (A/B)")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -315,6 +317,8 @@ def main():
     model.engine.use_x3 = not args.no_x3
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
+    if args.recompute_y128:
+        model.engine.recompute_y_couts = (64, 128)
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
 
     for _ in range(args.warmup):

@@ -114,14 +114,20 @@ def test_builder_api_and_inference_parity_cfg1():
                                                         (1, False, 0.0, "dice_loss", "auto"),
                                                         (1, True, 0.0, "iou_loss", "auto"),
                                                         (1, True, 0.0, "dice_loss", "always"),
-                                                        (1, True, 0.2, "dice_loss", "always")])
+                                                        (1, True, 0.2, "dice_loss", "always"),
+                                                        (1, True, 0.2, "dice_loss", "always+r128")])
 def test_train_step_parity(ncls, use_bn, drop, loss, fuse, record_property):
     """One train step against the oracle; fuse="always" runs the fused depthwise+pointwise
-    forward on every level it supports (32x32 and 16x16 here), "never" the split kernels."""
+    forward on every level it supports (32x32 and 16x16 here), "never" the split kernels;
+    "+r128": the 128-output blocks keep no y either (their weight gradients recompute it, through
+    dec2_block1's dropout view)."""
     from unet_amd.model import UNetModel
     from unet_amd.optim import AdamW
     n, hw = 2, 32
     model = UNetModel((hw, hw, 3), ncls, dropout_rate=drop, use_batch_norm=use_bn, seed=11)
+    if fuse.endswith("+r128"):
+        fuse = fuse[:-5]
+        model.engine.recompute_y_couts = (64, 128)
     model.engine.fuse_sepconv = fuse
     model.engine.fuse_bn_bwd = fuse != "never"  # "never": also the separate BN-backward dz pass
     orc = UNetOracle(ncls, drop, use_bn)

@@ -197,8 +197,9 @@ def test_train_step_128_batch4():
             assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name
 
 
-@pytest.mark.parametrize("fixture", ["train256.npz", "train256c21.npz"])
-def test_train_step_training_geometry(fixture):
+@pytest.mark.parametrize("fixture,recompute128", [("train256.npz", False), ("train256c21.npz", False),
+                                                  ("train256.npz", True)])
+def test_train_step_training_geometry(fixture, recompute128):
     """One train step at the geometry the reference trains at (scripts/train.py:84-88, 256x256)
     with configs[1]'s batch of 16 (binary) and configs[4]'s per-GPU batch of 8 (21 classes),
     against the committed float64 oracle step (tests/golden/make_golden.py train_big_fixture; the
@@ -216,6 +217,8 @@ def test_train_step_training_geometry(fixture):
     g = _load(fixture)
     size, n, ncls = int(g["size"]), int(g["n"]), int(g["ncls"])
     m = UNetModel((size, size, 3), ncls, dropout_rate=0.0)
+    if recompute128:  # the 128-output blocks keep no y either: unet_sepconv_bwd_filter recomputes it
+        m.engine.recompute_y_couts = (64, 128)
     w = MG.model_weights(ncls, MG.FULL, int(g["w_seed"]))
     m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
     x = MG.U(int(g["x_seed"]), (n, size, size, 3))

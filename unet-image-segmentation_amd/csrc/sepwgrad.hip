@@ -472,6 +472,199 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
     if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 16 * 16 + (tid % 16)]);
 }
 
+// Both weight gradients WITHOUT the data path (unet_sepconv_bwd_filter: dz and dy come from
+// memory), in the fused kernel's form: 4-wave blocks over 4 x 16 pixel tiles, two per CU, 64 or 128
+// outputs, dropout on the view.  Per tile: the view's halo and the dz tile -> LDS, y recomputed
+// with the forward's fmaf chain (taps from LDS) while the depthwise-filter gradient accumulates
+// against this thread's dy quads, then y^T dz by MFMA (wave w: ci 32 (w & 1) .., co quarters
+// 32 (CO/64 (w >> 1) + q) ..).  The next tile's halo / dz loads and dy quads are in flight meanwhile.
+template <int CO>
+struct Fw2Lds {
+    static constexpr int SIZE = fb::L_X + fb::L_YD + fb::PX * CO + fb::L_K;  // 77.3 KB (CO 128) / 61 KB (CO 64)
+    static_assert(fb::CI * CO <= SIZE && 9 * 16 * 16 * 4 <= SIZE, "epilogue scratch");
+    static_assert(2 * SIZE * 4 <= 160 * 1024, "two blocks per CU");
+};
+
+template <int MODE, bool DROP, int CO>
+__global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_filter2_kernel(SwArgs g) {
+    constexpr int TH = fb::TH, TW = fb::TW, HWp = fb::HWp, PX = fb::PX, NT = fb::NT, CI = fb::CI;
+    constexpr int NHQ = fb::NHQ, HR = fb::HR;
+    constexpr int DQ = PX * (CO / 4) / NT;  // dz float4 per thread per tile (4 / 8)
+    constexpr int NQW = CO / 64;            // (32 ci x 32 co) quarters per wave
+    __shared__ __attribute__((aligned(16))) float smem[Fw2Lds<CO>::SIZE];
+    float* Xs = smem;
+    float* Ys = Xs + fb::L_X;
+    float* Zs = Ys + fb::L_YD;
+    float* KS9 = Zs + PX * CO;  // the ci group's 9 taps [t][ci] (in LDS: registers go to the dz staging)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int j = blockIdx.x >> 3;  // XCD-aware (ci group, m-slice) map, as the fused kernel
+    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
+    const int c0 = CI * cig;
+    const int t_begin = slice * g.tps;
+    const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
+    const int tiles_h = g.H / TH;
+    const int C = g.x.C, Cin = g.Cin;
+    const int cq = tid & 15, ci = c0 + 4 * cq;
+
+    for (int e = tid; e < 9 * CI; e += NT) KS9[e] = g.dk[(e / CI) * Cin + c0 + e % CI];
+    const float* src = g.x.src0;
+    int cs = g.x.c0, cc = ci;
+    const float* scp = g.x.sc0;
+    const float* shp = g.x.sh0;
+    bool bn = MODE == UNET_VIEW_BNRELU;
+    if constexpr (MODE == UNET_VIEW_CONCAT) {
+        if (cc >= g.x.c0) {
+            src = g.x.src1;
+            cs = g.x.c1;
+            cc -= g.x.c0;
+            scp = g.x.sc1;
+            shp = g.x.sh1;
+            bn = true;
+        }
+    }
+    float4 hsc = f4(1.f), hsh = f4(0.f);
+    if constexpr (MODE != UNET_VIEW_PLAIN) {
+        if (bn) {
+            hsc = ld4(scp + cc);
+            hsh = ld4(shp + cc);
+        }
+    }
+    auto tile_base = [&](int T) {  // first pixel of tile T (column-major walk, th fastest)
+        const int th = T % tiles_h, r = T / tiles_h, tiles_w = g.W / TW;
+        return (int64_t)((r / tiles_w) * g.H + th * TH) * g.W + (r % tiles_w) * TW;
+    };
+    float4 hx[HR], rz[DQ], rdy[4];
+    // halo element k of this thread in tile T: its pixel index, or -1 outside the image (recomputed
+    // where needed instead of held in registers across the tile)
+    auto halo_px = [&](int T, int k) {
+        const int th = T % tiles_h, r = T / tiles_h, tiles_w = g.W / TW;
+        const int n = r / tiles_w, h0 = th * TH, w0 = (r % tiles_w) * TW;
+        const int e = tid + NT * k;
+        const int pix = e >> 4, rr = pix / HWp, c = pix - rr * HWp;
+        const int hh = h0 - 1 + rr, ww = w0 - 1 + c;
+        const bool ok = e < NHQ && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+        return ok ? (n * g.H + hh) * g.W + ww : -1;
+    };
+    auto load = [&](int T) {
+        const int th = T % tiles_h, r = T / tiles_h, tiles_w = g.W / TW;
+        const int n = r / tiles_w, h0 = th * TH, w0 = (r % tiles_w) * TW;
+#pragma unroll
+        for (int k = 0; k < HR; ++k) {
+            const int lp = halo_px(T, k);
+            hx[k] = ld4(src + ((int64_t)(lp < 0 ? 0 : lp) * cs + cc));
+        }
+        const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
+#pragma unroll
+        for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e / (CO/4), quad e % (CO/4)
+            const int e = tid + NT * k, p = e / (CO / 4), q = e % (CO / 4);
+            rz[k] = ld4(g.dz + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q);
+        }
+    };
+    auto load_dy = [&](int T) {  // this thread's dy quads: pixel (tid >> 4) + 16 k
+        const int64_t tb = tile_base(T);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = (tid >> 4) + 16 * k;
+            rdy[k] = ld4(g.dy + (tb + (int64_t)(p >> 4) * g.W + (p & 15)) * Cin + ci);
+        }
+    };
+    auto store = [&](int T) {
+#pragma unroll
+        for (int k = 0; k < HR; ++k) {
+            const int e = tid + NT * k;
+            const int lp = halo_px(T, k);
+            float4 v = hx[k];
+            if constexpr (MODE != UNET_VIEW_PLAIN) {
+                if (bn) v = bnrelu4(v, hsc, hsh);
+            }
+            if constexpr (DROP) {
+                const uint64_t i = (uint64_t)(lp < 0 ? 0 : lp) * C + ci;
+                v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
+            }
+            if (lp < 0) v = f4(0.f);
+            if (e < NHQ) *reinterpret_cast<float4*>(&Xs[(e >> 4) * CI + 4 * (e & 15)]) = v;
+        }
+#pragma unroll
+        for (int k = 0; k < DQ; ++k) {
+            const int e = tid + NT * k;
+            *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
+        }
+    };
+
+    const int wci = 32 * (wave & 1), wco = 32 * NQW * (wave >> 1);
+    floatx16 acc[NQW];
+#pragma unroll
+    for (int q = 0; q < NQW; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    float4 dwa[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) dwa[t] = f4(0.f);
+
+    if (t_begin < t_end) {
+        load(t_begin);
+        load_dy(t_begin);
+    }
+    for (int T = t_begin; T < t_end; ++T) {
+        store(T);
+        __syncthreads();
+        load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {  // (not unrolled: 9 taps in flight, not 36)
+            const int p = (tid >> 4) + 16 * k, pr = p >> 4, pc = p & 15;
+            const float4 dq = rdy[0];  // static register indexing: rotate the dy quads
+            rdy[0] = rdy[1];
+            rdy[1] = rdy[2];
+            rdy[2] = rdy[3];
+            float4 y = f4(0.f);
+#pragma unroll
+            for (int dy_ = 0; dy_ < 3; ++dy_)
+#pragma unroll
+                for (int dx_ = 0; dx_ < 3; ++dx_) {
+                    const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
+                    y = fma4(xv, *reinterpret_cast<const float4*>(&KS9[(dy_ * 3 + dx_) * CI + 4 * cq]), y);
+                    dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
+                }
+            *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
+        }
+        load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
+        __syncthreads();
+#pragma unroll 4
+        for (int s2 = 0; s2 < PX / 2; ++s2) {
+            const int p = 2 * s2 + hi;
+            const float a = Ys[p * CI + wci + lo];
+#pragma unroll
+            for (int q = 0; q < NQW; ++q)
+                acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Zs[p * CO + wco + 32 * q + lo], acc[q], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+    float* E = smem;  // pointwise slab rows c0 .. c0+63: [64 ci][CO]
+#pragma unroll
+    for (int q = 0; q < NQW; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) E[(wci + acc_row(r, hi)) * CO + wco + 32 * q + lo] = acc[q][r];
+    __syncthreads();
+    float* pw = g.pw_slab + ((int64_t)slice * Cin + c0) * CO;
+    for (int e = tid; e < CI * CO / 4; e += NT) st4(pw + 4 * e, *reinterpret_cast<const float4*>(&E[4 * e]));
+    __syncthreads();
+    float4* D = reinterpret_cast<float4*>(smem);  // [9][16 pixel rows][16 quads]
+#pragma unroll
+    for (int t = 0; t < 9; ++t) D[(t * 16 + (tid >> 4)) * 16 + cq] = dwa[t];
+    __syncthreads();
+    for (int o = 8; o > 0; o >>= 1) {
+        for (int e = tid; e < 9 * o * 16; e += NT) {
+            const int t = e / (o * 16), rr = (e / 16) % o, q = e % 16;
+            D[(t * 16 + rr) * 16 + q] = add4(D[(t * 16 + rr) * 16 + q], D[(t * 16 + rr + o) * 16 + q]);
+        }
+        __syncthreads();
+    }
+    float* dws = g.dw_slab + (int64_t)slice * 9 * Cin;
+    if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 16 * 16 + (tid % 16)]);
+}
+
 int resident_cus() {
     static int cus = 0;
     if (!cus) {
@@ -504,8 +697,8 @@ template <int MODE, bool DROP>
 void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
     if (a.da_dl) sepconv_bwd_fused_kernel<MODE, true><<<blocks, fb::NT, 0, st>>>(a);
     else if (a.da) sepconv_bwd_fused_kernel<MODE><<<blocks, fb::NT, 0, st>>>(a);
-    else if (cout == 128) sepconv_wgrad_kernel<MODE, DROP, 128><<<blocks, NT, 0, st>>>(a);
-    else sepconv_wgrad_kernel<MODE, DROP, 64><<<blocks, NT, 0, st>>>(a);
+    else if (cout == 128) sepconv_bwd_filter2_kernel<MODE, DROP, 128><<<blocks, fb::NT, 0, st>>>(a);
+    else sepconv_bwd_filter2_kernel<MODE, DROP, 64><<<blocks, fb::NT, 0, st>>>(a);
 }
 
 }  // namespace
@@ -529,8 +722,7 @@ extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int 
 extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout) {
     if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || (cout != 64 && cout != 128) || h % TH || w % TW)
         return 0;
-    // the larger of the two plans (the fused block backward, 64 outputs, runs twice the slices)
-    const SwPlan p = sw_plan(n, h, w, cin, cout == 64);
+    const SwPlan p = sw_plan(n, h, w, cin, true);
     return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
 }
 
@@ -540,7 +732,7 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
     const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w, cin, a.da || a.da_dl);
+    const SwPlan p = sw_plan(n, h, w, cin, true);
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;

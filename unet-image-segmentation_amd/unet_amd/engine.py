@@ -35,11 +35,11 @@ DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
 
 
 FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools/bench_sepconv.py sweeps)
-RECOMPUTE_Y_COUT = 64      # fused y-recomputing weight gradient for 64-output blocks only (r2 step A/B)
+RECOMPUTE_Y_COUTS = (64,)  # blocks whose weight gradients recompute y (64 outputs: the fused block backward)
 
 
 def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bool, fuse: str = "auto",
-                     recompute_y: bool = True):
+                     recompute_y: bool = True, recompute_couts=RECOMPUTE_Y_COUTS):
     """The kernels a conv_block forward runs: (fused, keep_y).  fused: one unet_sepconv_fwd launch
     (else unet_dwconv3x3_fwd + unet_pointwise_fwd, which always store y); keep_y: the fused launch
     also stores the depthwise output y for the weight gradients (training blocks whose weight
@@ -47,7 +47,7 @@ def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bo
     want = fuse == "always" or (fuse == "auto" and h * w >= FUSE_MIN_PIXELS)
     if not (want and ops.sepconv_supported(view, n, h, w, cout)):
         return False, training
-    y_recompute = training and recompute_y and cout == RECOMPUTE_Y_COUT and \
+    y_recompute = training and recompute_y and cout in recompute_couts and \
         ops.sepconv_bwd_filter_supported(view, n, h, w, cout)
     return True, training and not y_recompute
 
@@ -178,6 +178,7 @@ class UNetEngine:
         # depthwise output y from the block's input view (unet_sepconv_bwd_filter), so their
         # forward never stores y
         self.recompute_y = os.environ.get("UNET_RECOMPUTE_Y", "1") != "0"
+        self.recompute_y_couts = RECOMPUTE_Y_COUTS
         # issue a y-recomputing block's fused weight gradient (one 111 KB-LDS block per CU for the
         # launch's whole length) only after the main stream has issued the NEXT block's statistics
         # finish, instead of beside its own depthwise data gradient (under data parallelism the
@@ -321,7 +322,8 @@ class UNetEngine:
         bb = A.blocks[b.name]
         gamma, beta, mm, mv = self._bn(b.name)
         dk, pk = self._wts(b)
-        fused, keep_y = block_fwd_choice(view, n, h, w, b.cout, training, self.fuse_sepconv, self.recompute_y)
+        fused, keep_y = block_fwd_choice(view, n, h, w, b.cout, training, self.fuse_sepconv, self.recompute_y,
+                                         self.recompute_y_couts)
         if fused:
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view
