@@ -1,53 +1,30 @@
-// Weight gradients of a C -> 64 (or 128) SeparableConv2D (reference model/u_net.py:14-20; the pixel
-// reductions of Keras' implicit backward, scripts/train.py:308) in ONE pass that never reads the
-// depthwise output y:
+// Backward passes of a SeparableConv2D block that recompute the depthwise output y instead of
+// reading it (reference model/u_net.py:14-25; the GradientTape of scripts/train.py:308):
 //
 //   d_pw[ci][co] = sum_px y[px][ci] dz[px][co]          y = depthwise3x3(x), recomputed here
 //   d_dw[t][ci]  = sum_px x[px + off(t)][ci] dy[px][ci]  (the 3x3 taps y is formed from)
 //
-// x is the block's input VIEW (BN affine + ReLU / concat / dropout on load, zero padding).  These
-// are the 256 x 256 level's conv blocks (enc1_block2, dec1_block2), HBM-bound: the separate route
-// (unet_pointwise_bwd_filter over a stored y, then unet_dwconv3x3_bwd_filter over (x, dy)) moves
-// y twice (forward store + read) and x once more.  Here the forward keeps no y, and the backward
-// streams x, dz and dy once: 768 B per pixel.
-//
-// One block (8 waves) per CU walks a contiguous run of 8 x 16 pixel tiles.  Per tile:
-//   * the 10 x 18 halo of the view (64 channels) and the dz tile -> LDS (register staged: the next
-//     tile's loads are in flight while this one computes); each thread's dy quads -> registers
-//     (loaded once this tile's filter-gradient FMAs have consumed the previous ones);
-//   * every thread evaluates 4 (pixel, 4-channel) quads of y from 9 conflict-free ds_read_b128
-//     taps with the forward's k-ordered fmaf chain (y bitwise equal to unet_sepconv_fwd's) into
-//     the LDS y tile, and accumulates the depthwise filter gradient from the same taps;
-//   * wave w runs v_mfma_f32_32x32x2_f32 for its 32 x 32 (ci, co) quarter over half the tile's
-//     pixels (A = y^T, B = dz: one conflict-free ds_read_b32 each per MFMA).
-// The two pixel halves of each quarter and the 32 threads per channel quad of the filter gradient
-// are combined in fixed order; one slab per block, reduced by reduce_slabs in fixed order.
-// The train step runs the fused block backward further down (sepconv_bwd_fused_kernel) instead of
-// this kernel; unet_sepconv_bwd_filter stays in the ABI (tested, and the route for a caller that
-// has dz and dy already).
+// x is the block's input VIEW (BN affine + ReLU / concat / dropout on load, zero padding).
+//   * sepconv_bwd_fused_kernel (unet_sepconv_bwd_fused): the whole backward of a 64-output block
+//     but its depthwise data gradient -- dz formed per tile from (da, z), dy = dz . pk^T, both
+//     weight gradients; the train step's path for the 256 x 256 level (HBM-bound: the forward
+//     keeps no y, dz never goes to memory);
+//   * sepconv_bwd_filter2_kernel (unet_sepconv_bwd_filter): both weight gradients from dz and dy
+//     in memory, 64 or 128 outputs.
+// Both run 4-wave blocks over 4 x 16 pixel tiles, two blocks per CU; each block walks a run of
+// tiles, one fixed-order slab per block, reduced by reduce_slabs in fixed order.
 #include "common.h"
 #include "view.h"
 
 namespace unet {
 namespace {
 
-#ifndef SW_KO  // lab knock-outs (tools/lab/sw_lab.hip, sw_fused_lab.hip): 1 MFMA, 2 depthwise VALU, 4 loop loads,
-               // 8 LDS staging, 16 the fused dy GEMM, 32 the fused dy store
+#ifndef SW_KO  // lab knock-outs (tools/lab/sw_fused_lab.hip): 1 weight-gradient MFMA, 2 depthwise VALU,
+               // 4 loads of the next tile, 8 LDS staging, 16 the dy MFMA, 32 the dy store
 #define SW_KO 0
 #endif
-constexpr int TH = 8, TW = 16, HWp = TW + 2, HPIX = (TH + 2) * HWp;  // 180 halo pixels
-constexpr int CI = 64;                                                // input channels per block (ci group)
-constexpr int NT = 512;                                               // threads
-constexpr int NHQ = HPIX * (CI / 4);                                  // halo float4 (2880)
-constexpr int HR = (NHQ + NT - 1) / NT;                               // per thread (6)
-constexpr int LDS_HALO = HPIX * CI, LDS_YT = 128 * CI;
-template <int CO>
-struct SwLds {
-    static constexpr int SIZE = LDS_HALO + LDS_YT + 128 * CO;  // 110 KB (CO 64) / 142 KB (CO 128)
-    static_assert(64 * 64 * 2 <= SIZE && 9 * 32 * 16 * 4 <= SIZE, "epilogue scratch");
-    static_assert(SIZE * 4 <= 160 * 1024, "LDS");
-};
-
+constexpr int TH = 8, TW = 16;  // shape granularity of the C-ABI (h % 8, w % 16)
+constexpr int CI = 64;          // input channels per block (ci group)
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
 struct SwArgs {
@@ -68,188 +45,6 @@ struct SwArgs {
     const float *da_dl, *da_k;  // rank-one da = da_dl[px] * da_k[c] (the binary head), da NULL
     float* dy_out;
 };
-
-template <int MODE, bool DROP, int CO>
-__global__ __launch_bounds__(NT, 1) void sepconv_wgrad_kernel(SwArgs g) {
-    constexpr int DQ = 128 * CO / 4 / NT;  // dz float4 per thread per tile (4 / 8)
-    constexpr int NQ = 2 * (CO / 32);      // (32 ci x 32 co) quarters of the block's 64 x CO output
-    constexpr int PP = 8 / NQ;             // waves per quarter (pixel parts of the tile)
-    constexpr int KS = 64 / PP;            // MFMA k-steps (pixel pairs) per wave per tile
-    using L = SwLds<CO>;
-    constexpr int ZS = CO;
-    __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
-    float* Xs = smem;
-    float* Ys = smem + LDS_HALO;
-    float* Zs = smem + LDS_HALO + LDS_YT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int lo = lane & 31, hi = lane >> 5;
-    // XCD-aware block -> (ci group, m-slice): blocks b and b + 8 run on one XCD; the ci groups of
-    // an m-slice get consecutive j = b >> 3 there, so they share its dz tiles through that L2
-    const int j = blockIdx.x >> 3;
-    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
-    const int c0 = CI * cig;
-    const int t_begin = slice * g.tps;
-    const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
-    const int tiles_w = g.W / TW, tiles_h = g.H / TH;
-    const int C = g.x.C, Cin = g.Cin;
-
-    // this thread's channel quad (halo staging, y and filter-gradient quads alike)
-    const int cq = tid & 15, ci = c0 + 4 * cq;
-    float4 kt[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) kt[t] = ld4(g.dk + t * Cin + ci);
-    const float* src = g.x.src0;
-    int cs = g.x.c0, cc = ci;
-    const float* scp = g.x.sc0;
-    const float* shp = g.x.sh0;
-    bool bn = MODE == UNET_VIEW_BNRELU;
-    if constexpr (MODE == UNET_VIEW_CONCAT) {
-        if (cc >= g.x.c0) {
-            src = g.x.src1;
-            cs = g.x.c1;
-            cc -= g.x.c0;
-            scp = g.x.sc1;
-            shp = g.x.sh1;
-            bn = true;
-        }
-    }
-    float4 hsc = f4(1.f), hsh = f4(0.f);
-    if constexpr (MODE != UNET_VIEW_PLAIN) {
-        if (bn) {
-            hsc = ld4(scp + cc);
-            hsh = ld4(shp + cc);
-        }
-    }
-
-    float4 hx[HR], rz[DQ], rdy[4];
-    int lp[HR];
-    auto load = [&](int T) {
-        const int tw = T % tiles_w, r0 = T / tiles_w;
-        const int h0 = (r0 % tiles_h) * TH, n = r0 / tiles_h, w0 = tw * TW;
-#pragma unroll
-        for (int k = 0; k < HR; ++k) {
-            const int e = tid + NT * k;
-            const int pix = e >> 4, r = pix / HWp, c = pix - r * HWp;
-            const int hh = h0 - 1 + r, ww = w0 - 1 + c;
-            const bool ok = e < NHQ && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
-            lp[k] = ok ? (n * g.H + hh) * g.W + ww : -1;
-            hx[k] = ld4(src + ((int64_t)(ok ? lp[k] : 0) * cs + cc));
-        }
-        const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
-#pragma unroll
-        for (int k = 0; k < DQ; ++k) {  // dz tile: element e = pixel e / (CO/4), quad e % (CO/4)
-            const int e = tid + NT * k, p = e / (CO / 4), q = e % (CO / 4);
-            const int64_t o = (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * CO + 4 * q;
-            rz[k] = ld4(g.dz + o);
-        }
-    };
-    auto load_dy = [&](int T) {  // dy of this thread's quads: pixel (tid >> 4) + 32 k
-        const int tw = T % tiles_w, r0 = T / tiles_w;
-        const int h0 = (r0 % tiles_h) * TH, n = r0 / tiles_h, w0 = tw * TW;
-        const int64_t mbase = (int64_t)(n * g.H + h0) * g.W + w0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int p = (tid >> 4) + 32 * k;
-            rdy[k] = ld4(g.dy + (mbase + (int64_t)(p >> 4) * g.W + (p & 15)) * Cin + ci);
-        }
-    };
-    auto store = [&]() {
-#pragma unroll
-        for (int k = 0; k < HR; ++k) {
-            const int e = tid + NT * k;
-            float4 v = hx[k];
-            if constexpr (MODE != UNET_VIEW_PLAIN) {
-                if (bn) v = bnrelu4(v, hsc, hsh);
-            }
-            if constexpr (DROP) {
-                const uint64_t i = (uint64_t)(lp[k] < 0 ? 0 : lp[k]) * C + ci;
-                v = mul4(v, drop_mult4(g.x.seed, i, g.x.rate, g.x.inv_keep));
-            }
-            if (lp[k] < 0) v = f4(0.f);
-            if (e < NHQ) *reinterpret_cast<float4*>(&Xs[(e >> 4) * CI + 4 * (e & 15)]) = v;
-        }
-#pragma unroll
-        for (int k = 0; k < DQ; ++k) {
-            const int e = tid + NT * k;
-            *reinterpret_cast<float4*>(&Zs[(e / (CO / 4)) * CO + 4 * (e % (CO / 4))]) = rz[k];
-        }
-    };
-
-    // MFMA quarter of this wave: ci rows 32 (q & 1) .., co columns 32 (q >> 1) .. of q = w % NQ,
-    // over pixel part w / NQ of the tile (KS k-steps of 2 pixels)
-    const int qd = wave % NQ;
-    const int wci = 32 * (qd & 1), wco = 32 * (qd >> 1), wpx = 2 * KS * (wave / NQ);
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float4 dwa[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) dwa[t] = f4(0.f);
-
-    if (t_begin < t_end) {
-        load(t_begin);
-        load_dy(t_begin);
-    }
-    for (int T = t_begin; T < t_end; ++T) {
-        if constexpr (!(SW_KO & 8)) store();
-        __syncthreads();
-        if constexpr (!(SW_KO & 4)) load(T + 1 < t_end ? T + 1 : T);  // next tile in flight (past the end: a valid, unused tile)
-#pragma unroll 1
-        for (int k = 0; k < ((SW_KO & 2) ? 0 : 4); ++k) {  // (not unrolled: 9 taps in flight, not 36)
-            const int p = (tid >> 4) + 32 * k, pr = p >> 4, pc = p & 15;
-            const float4 dq = rdy[0];  // static register indexing: rotate the dy quads
-            rdy[0] = rdy[1];
-            rdy[1] = rdy[2];
-            rdy[2] = rdy[3];
-            float4 y = f4(0.f);
-#pragma unroll
-            for (int dy_ = 0; dy_ < 3; ++dy_)
-#pragma unroll
-                for (int dx_ = 0; dx_ < 3; ++dx_) {
-                    const float4 xv = *reinterpret_cast<const float4*>(&Xs[((pr + dy_) * HWp + pc + dx_) * CI + 4 * cq]);
-                    y = fma4(xv, kt[dy_ * 3 + dx_], y);
-                    dwa[dy_ * 3 + dx_] = fma4(xv, dq, dwa[dy_ * 3 + dx_]);
-                }
-            *reinterpret_cast<float4*>(&Ys[p * CI + 4 * cq]) = y;
-        }
-        if constexpr (!(SW_KO & 4)) load_dy(T + 1 < t_end ? T + 1 : T);  // its latency hides behind the MFMA phase
-        __syncthreads();
-#pragma unroll 4
-        for (int s = 0; s < ((SW_KO & 1) ? 0 : KS); ++s) {
-            const int p = wpx + 2 * s + hi;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ys[p * CI + wci + lo], Zs[p * ZS + wco + lo], acc, 0, 0, 0);
-        }
-        __syncthreads();
-    }
-
-    // pointwise slab rows c0 .. c0+63: the PP pixel parts of each quarter, fixed order
-    float* E = smem;  // [PP][64 ci][CO]
-#pragma unroll
-    for (int r = 0; r < 16; ++r) E[((wave / NQ) * CI + wci + acc_row(r, hi)) * CO + wco + lo] = acc[r];
-    __syncthreads();
-    float* pw = g.pw_slab + ((int64_t)slice * Cin + c0) * CO;
-    for (int e = tid; e < CI * CO / 4; e += NT) {
-        float4 a = *reinterpret_cast<const float4*>(&E[4 * e]);
-#pragma unroll
-        for (int pp = 1; pp < PP; ++pp) a = add4(a, *reinterpret_cast<const float4*>(&E[pp * CI * CO + 4 * e]));
-        st4(pw + 4 * e, a);
-    }
-    __syncthreads();
-    // depthwise slab [t][ci]: the 32 threads of each channel quad, fixed-order tree
-    float4* D = reinterpret_cast<float4*>(smem);  // [9][32 pixel rows][16 quads]
-#pragma unroll
-    for (int t = 0; t < 9; ++t) D[(t * 32 + (tid >> 4)) * 16 + cq] = dwa[t];
-    __syncthreads();
-    for (int o = 16; o > 0; o >>= 1) {
-        for (int e = tid; e < 9 * o * 16; e += NT) {
-            const int t = e / (o * 16), rr = (e / 16) % o, q = e % 16;
-            D[(t * 32 + rr) * 16 + q] = add4(D[(t * 32 + rr) * 16 + q], D[(t * 32 + rr + o) * 16 + q]);
-        }
-        __syncthreads();
-    }
-    float* dws = g.dw_slab + (int64_t)slice * 9 * Cin;
-    if (tid < 9 * 16) st4(dws + (tid / 16) * Cin + c0 + 4 * (tid % 16), D[(tid / 16) * 32 * 16 + (tid % 16)]);
-}
 
 // ------------------------------------------------------------------------------------------
 // The fused block backward (unet_sepconv_bwd_fused): the whole backward of a 64-output conv block
@@ -679,14 +474,14 @@ int resident_cus() {
 struct SwPlan {
     int tiles, ncig, S, tps;
 };
-SwPlan sw_plan(int n, int h, int w, int cin, bool fused = false) {
+SwPlan sw_plan(int n, int h, int w, int cin) {
     SwPlan p;
-    p.tiles = fused ? n * (h / fb::TH) * (w / fb::TW) : n * (h / TH) * (w / TW);
+    p.tiles = n * (h / fb::TH) * (w / fb::TW);
     p.ncig = cin / CI;
-    // filter-only kernel: one block per CU (110-142 KB of LDS); fused block backward: two per CU.
-    // m-slices a multiple of 8 (the XCD map).  (128 / 192 blocks, leaving CUs to the main stream,
-    // measured -1.7 / -0.3 % img/s.)
-    int S = (int)cdiv((fused ? 2 : 1) * resident_cus(), p.ncig);
+    // two blocks per CU (77 KB of LDS each), m-slices a multiple of 8 (the XCD map).  (Fewer blocks,
+    // leaving CUs to the main stream: -1.7 / -0.3 % img/s in round 2; 2-8x as many, finer runs:
+    // no gain, profiles/r3m_fb_split_ab.log.)
+    int S = (int)cdiv(2 * resident_cus(), p.ncig);
     S = (int)cdiv(S, 8) * 8;
     p.tps = (int)cdiv(p.tiles, S);
     p.S = S;
@@ -722,7 +517,7 @@ extern "C" int unet_sepconv_bwd_filter_supported(const unet_view* x, int n, int 
 extern "C" size_t unet_sepconv_bwd_filter_workspace(int n, int h, int w, int cin, int cout) {
     if (n <= 0 || h <= 0 || w <= 0 || cin <= 0 || cin % CI || (cout != 64 && cout != 128) || h % TH || w % TW)
         return 0;
-    const SwPlan p = sw_plan(n, h, w, cin, true);
+    const SwPlan p = sw_plan(n, h, w, cin);
     return align_up((size_t)p.S * cin * cout * sizeof(float), 256) + align_up((size_t)p.S * 9 * cin * sizeof(float), 256);
 }
 
@@ -732,7 +527,7 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
     const int cin = x->c0 + (x->mode == UNET_VIEW_CONCAT ? x->c1 : 0);
     const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
     UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", op, ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w, cin, true);
+    const SwPlan p = sw_plan(n, h, w, cin);
     a.x = make_dview(*x);
     a.N = n;
     a.H = h;
