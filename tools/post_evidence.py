@@ -44,6 +44,11 @@ def main():
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), fe, wr,
                                 os.path.join(P, f"{tag}_traffic_{op[5:]}.json"), op], capture_output=True, text=True)
             print(op, r.stdout.strip()[:200], r.stderr.strip()[-200:])
+    if fe and wr:  # whole-step HBM bytes (every dispatch of the PMC passes' timed steps)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_step_bytes.py"), fe, wr,
+                            os.path.join(G, "bench.log"), os.path.join(P, f"{tag}_step_traffic.json")],
+                           capture_output=True, text=True)
+        print("step traffic", r.stdout.strip()[:200], r.stderr.strip()[-300:])
     # enc2_block1 forward at batch 32: bytes and the SQ stall group, averaged over its dispatches
     rec = {}
     for kind in ("fetch", "write", "sq"):
