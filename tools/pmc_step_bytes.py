@@ -34,7 +34,8 @@ def main():
         nsteps = min(3, len(ends))
         res[kind + "_bytes_per_step"] = sum(disp[i] for i in sel) / nsteps
         for i in sel:
-            k = names[i].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
+            k = names[i].replace("(anonymous namespace)", "").replace("void ", "").split("(")[0]
+            k = k.split("<")[0].split("::")[-1] + ("<" + k.split("<", 1)[1][:24] if "<" in k else "")
             fam[k][0 if kind == "read" else 1] += disp[i] / nsteps
     line = next(json.loads(l) for l in open(bench) if l.startswith("{"))
     ms = line["ms_per_step"]

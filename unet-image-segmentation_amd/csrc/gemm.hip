@@ -62,6 +62,32 @@ struct RowsArgs {
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
+// XCD-aware placement: workgroups go to the 8 XCDs round-robin by linear id (x fastest), and each
+// XCD has its own L2.  For a (groups x sibs) grid whose sibling blocks read the same operand rows
+// (the N-tiles of one row tile, the (p, q) tiles of one m-slice), renumber the linear id so that
+// all siblings of a group run on one XCD and share those rows through its L2 instead of each
+// fetching them from HBM.  Needs groups % 8 == 0 (else the grid order is kept); same tiles, same
+// arithmetic -- only where each tile runs changes.  grid x = groups, y = sibs.
+__device__ __forceinline__ void xcd_group_order(int groups, int sibs, int& grp, int& sib) {
+    grp = blockIdx.x;
+    sib = blockIdx.y;
+    if (sibs > 1 && (groups & 7) == 0) {
+        const int L = blockIdx.x + blockIdx.y * groups, u = L >> 3;
+        grp = (u / sibs) * 8 + (L & 7);
+        sib = u % sibs;
+    }
+}
+// the same with the siblings along grid x (the weight-gradient GEMMs: x = (p, q) tile, y = m-slice)
+__device__ __forceinline__ void xcd_group_order_sx(int sibs, int groups, int& sib, int& grp) {
+    sib = blockIdx.x;
+    grp = blockIdx.y;
+    if (sibs > 1 && (groups & 7) == 0) {
+        const int L = blockIdx.x + blockIdx.y * sibs, u = L >> 3;
+        grp = (u / sibs) * 8 + (L & 7);
+        sib = u % sibs;
+    }
+}
+
 template <int BM, int BN, int AMODE, bool DROP, int EPI>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(RowsArgs g) {
     constexpr int LDA = BM + 4, LDB = BN + 4;
@@ -465,8 +491,10 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int lo = lane & 31, hi = lane >> 5;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    int mt, nt;  // row tile, column tile (the N-tiles of a row tile share its A rows through one L2)
+    xcd_group_order(gridDim.x, gridDim.y, mt, nt);
+    const int m0 = mt * BM;
+    const int n0 = nt * BN;
     const int M_rem = (g.M - m0) < BM ? (int)(g.M - m0) : BM;
     const int K = g.K;
 
@@ -568,7 +596,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             }
             if (!kv || aoff[r] < 0) v = f4(0.f);
             if constexpr (AMODE == A_BNBWD) {
-                if (g.side && blockIdx.y == 0 && kv && aoff[r] >= 0) st4(g.side + aoff[r] + ak, v);
+                if (g.side && nt == 0 && kv && aoff[r] >= 0) st4(g.side + aoff[r] + ak, v);
             }
             const int row = arow + (256 / KQ) * r;
             if constexpr (X6) {
@@ -744,7 +772,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                     o.x = a.x + d * f;
                     o.y = a.y + b.y + d * d * na * f;
                 }
-                if (n < g.N) g.stats[(int64_t)blockIdx.x * g.N + n] = o;
+                if (n < g.N) g.stats[(int64_t)mt * g.N + n] = o;
             }
         }
     }
@@ -784,7 +812,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         }
         __syncthreads();
         if (wm == 0 && hi == 0) {
-            float* out = g.bnpart + (int64_t)blockIdx.x * 2 * g.N;
+            float* out = g.bnpart + (int64_t)mt * 2 * g.N;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int col = wn * (BN / 2) + tn * 32 + lo;
@@ -858,9 +886,11 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     const int wp = wave >> 1, wq = wave & 1;
     const int lo = lane & 31, hi = lane >> 5;
     const int ntp = (g.P + BP - 1) / BP;
-    const int p0 = (blockIdx.x % ntp) * BP;
-    const int q0 = (blockIdx.x / ntp) * BQ;
-    const int mb = (int)(blockIdx.y * g.mslice);
+    int tile, slice;  // the (p, q) tiles of an m-slice read the same y / dz rows: one XCD's L2
+    xcd_group_order_sx(gridDim.x, gridDim.y, tile, slice);
+    const int p0 = (tile % ntp) * BP;
+    const int q0 = (tile / ntp) * BQ;
+    const int mb = (int)(slice * g.mslice);
     const int me = (int)((mb + g.mslice) < g.M ? (mb + g.mslice) : g.M);
     const bool roleA = !X6 || tid < 128, roleB = !X6 || tid >= 128;
     const int unit = tid & 127;
@@ -967,7 +997,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
             }
         }
     };
-    const bool csum_on = g.colpart != nullptr && (int)blockIdx.x < ntp;  // q-tile 0 blocks sum A's columns
+    const bool csum_on = g.colpart != nullptr && tile < ntp;  // q-tile 0 blocks sum A's columns
     float4 csum = f4(0.f);
     // X6: 4 consecutive m (rows r = 0..3) of channel c of the thread's quad, split, into the planes
     auto store_t4 = [&](unsigned short* base, int rows, const float4* rv) {
@@ -1066,15 +1096,15 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
             if (tid < PQ && p0 + 4 * tid < g.P) {
                 float4 t = T[4 * tid];
                 for (int j = 1; j < 4; ++j) t = add4(t, T[4 * tid + j]);
-                st4(g.colpart + (int64_t)blockIdx.y * g.P + p0 + 4 * tid, t);
+                st4(g.colpart + (int64_t)slice * g.P + p0 + 4 * tid, t);
             }
         } else if (tid < PQ && pv) {
             float4 t = T[tid];
             for (int j = 1; j < AS; ++j) t = add4(t, T[j * PQ + tid]);
-            st4(g.colpart + (int64_t)blockIdx.y * g.P + p, t);
+            st4(g.colpart + (int64_t)slice * g.P + p, t);
         }
     }
-    float* slab = g.slab + (int64_t)blockIdx.y * g.P * g.Q;
+    float* slab = g.slab + (int64_t)slice * g.P * g.Q;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
