@@ -118,6 +118,15 @@ __device__ __forceinline__ void stage(float4* T, const DView& v, int n, int h0, 
     }
 }
 
+// XCD-aware tile order: workgroups go to the 8 XCDs round-robin by linear id, so neighbouring tiles
+// (which re-read each other's halo rows and columns) would each run on a different XCD, i.e. behind a
+// different L2.  With the tile count a multiple of 8, XCD x instead takes the contiguous run of tiles
+// [x T/8, (x+1) T/8) in order: a tile's neighbours are resident on the same XCD and its halo reads
+// hit that L2.  Same tiles, same arithmetic, same per-tile slabs -- only the placement changes.
+__device__ __forceinline__ int xcd_tile(int b, int tiles) {
+    return (tiles & 7) == 0 ? (b & 7) * (tiles >> 3) + (b >> 3) : b;
+}
+
 __device__ __forceinline__ void tile_coords(int b, int tiles_w, int tiles_h, int TW, int& n, int& h0, int& w0) {
     const int tw = b % tiles_w;
     b /= tiles_w;
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(256, 3) void dw_tile_fwd(DView v, int N, int H, int
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
     int n, h0, w0;
-    tile_coords(blockIdx.x, tiles_w, tiles_h, G::TW, n, h0, w0);
+    tile_coords(xcd_tile(blockIdx.x, gridDim.x), tiles_w, tiles_h, G::TW, n, h0, w0);
     const int cbase = blockIdx.y * 4 * QT;
     stage<MODE, DROP, QT>(T, v, n, h0, w0, H, W, cbase);
     const int q = threadIdx.x % QT, col = threadIdx.x / QT;
@@ -183,7 +192,8 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
     int n, h0, w0;
-    tile_coords(blockIdx.x, tiles_w, tiles_h, G::TW, n, h0, w0);
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    tile_coords(tile, tiles_w, tiles_h, G::TW, n, h0, w0);
     const int cbase = blockIdx.y * 4 * QT;
     const int C = v.C;
     DView dv{};
@@ -296,7 +306,7 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
         }
     }
     if constexpr (STATS) {  // fixed-order reduction over the TW column lanes of each channel quad
-        float* out = bnpart + (int64_t)blockIdx.x * 2 * C;
+        float* out = bnpart + (int64_t)tile * 2 * C;
         __syncthreads();
         T[threadIdx.x] = s1;
         __syncthreads();

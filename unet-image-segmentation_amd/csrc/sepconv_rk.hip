@@ -72,7 +72,10 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
     const int tiles_w = g.W / TW, tiles_h = g.H / TH;
-    int t = blockIdx.x;
+    // pixel tile: XCD-contiguous order (neighbouring tiles re-read each other's halo through one L2;
+    // the tile count is a multiple of 8 on every level the fused forward runs)
+    const int tile = (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    int t = tile;
     const int tw = t % tiles_w;
     t /= tiles_w;
     const int th = t % tiles_h;
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
                 const int cl = tn * 32 + lo;
                 const int col = n0 + cl;
                 if (col < g.Cout)
-                    g.stats[(int64_t)blockIdx.x * g.Cout + col] =
+                    g.stats[(int64_t)tile * g.Cout + col] =
                         make_float2(mean[tn], (red[cl] + red[BN + cl]) + (red[2 * BN + cl] + red[3 * BN + cl]));
             }
         }
