@@ -339,7 +339,14 @@ __global__ __launch_bounds__(256, 2) void dw_tile_bwd_filter(DView v, int N, int
     float4 acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t] = f4(0.f);
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // XCD-contiguous assignment (as xcd_tile): XCD x walks tiles [x T/8, (x+1) T/8), its blocks
+    // interleaved over that run, so neighbouring tiles' halos meet in one L2.  The block's slab and
+    // the fixed-order slab sum stay as they were; only which tiles a slab sums changes
+    const bool xo = (ntiles & 7) == 0 && (gridDim.x & 7) == 0;
+    const int run = xo ? ntiles >> 3 : ntiles, base = xo ? (int)(blockIdx.x & 7) * run : 0;
+    const int step = xo ? (int)(gridDim.x >> 3) : (int)gridDim.x;
+    for (int i = xo ? (int)(blockIdx.x >> 3) : (int)blockIdx.x; i < run; i += step) {
+        const int tile = base + i;
         int n, h0, w0;
         tile_coords(tile, tiles_w, tiles_h, G::TW, n, h0, w0);
         const int w = w0 + col;
