@@ -83,8 +83,10 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
     float* KS9 = Wt + fb::L_W;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
-    const int j = blockIdx.x >> 3;  // XCD-aware (ci group, m-slice) map, as sepconv_wgrad_kernel
-    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
+    const int j = blockIdx.x >> 3;  // XCD-aware (ci group, m-slice) map: the ci groups of a slice share an XCD
+    // slices contiguous per XCD: XCD x runs slices [x S/8, (x+1) S/8), i.e. neighbouring tile columns,
+    // so their shared halo columns meet in one L2 (S = gridDim.x / ncig, a multiple of 8)
+    const int cig = j % g.ncig, slice = (int)(blockIdx.x & 7) * (int)(gridDim.x / g.ncig / 8) + j / g.ncig;
     const int c0 = CI * cig;
     const int t_begin = slice * g.tps;
     const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
@@ -294,7 +296,9 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_filter2_kernel(SwArgs g
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int lo = lane & 31, hi = lane >> 5;
     const int j = blockIdx.x >> 3;  // XCD-aware (ci group, m-slice) map, as the fused kernel
-    const int cig = j % g.ncig, slice = (j / g.ncig) * 8 + (blockIdx.x & 7);
+    // slices contiguous per XCD: XCD x runs slices [x S/8, (x+1) S/8), i.e. neighbouring tile columns,
+    // so their shared halo columns meet in one L2 (S = gridDim.x / ncig, a multiple of 8)
+    const int cig = j % g.ncig, slice = (int)(blockIdx.x & 7) * (int)(gridDim.x / g.ncig / 8) + j / g.ncig;
     const int c0 = CI * cig;
     const int t_begin = slice * g.tps;
     const int t_end = t_begin + g.tps < g.tiles ? t_begin + g.tps : g.tiles;
