@@ -284,6 +284,8 @@ def main():
                     help="fused conv forward on the levels >= 64x64 (auto) or on every level (A/B)")
     ap.add_argument("--recompute-y128", action="store_true",
                     help="128-output blocks too: no y store, weight gradients recompute it (A/B)")
+    ap.add_argument("--recompute-y64-128", action="store_true",
+                    help="the 64 -> 128 block (enc2_block1) too: no y store, recomputed (A/B)")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -319,6 +321,8 @@ def main():
     model.engine.fuse_sepconv = args.fuse
     if args.recompute_y128:
         model.engine.recompute_y_couts = (64, 128)
+    elif args.recompute_y64_128:
+        model.engine.recompute_y_couts = (64, (64, 128))
     x, y = synthetic_batch(args.batch, args.size, args.size, args.num_classes, 2301 + rank, device)
 
     for _ in range(args.warmup):

@@ -35,7 +35,9 @@ DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
 
 
 FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools/bench_sepconv.py sweeps)
-RECOMPUTE_Y_COUTS = (64,)  # blocks whose weight gradients recompute y (64 outputs: the fused block backward)
+# blocks whose weight gradients recompute y instead of the forward storing it: an output channel count
+# (64: the fused block backward), or an (input, output) channel pair
+RECOMPUTE_Y_COUTS = (64,)
 
 
 def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bool, fuse: str = "auto",
@@ -47,7 +49,7 @@ def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bo
     want = fuse == "always" or (fuse == "auto" and h * w >= FUSE_MIN_PIXELS)
     if not (want and ops.sepconv_supported(view, n, h, w, cout)):
         return False, training
-    y_recompute = training and recompute_y and cout in recompute_couts and \
+    y_recompute = training and recompute_y and (cout in recompute_couts or (view.channels, cout) in recompute_couts) and \
         ops.sepconv_bwd_filter_supported(view, n, h, w, cout)
     return True, training and not y_recompute
 
