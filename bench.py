@@ -280,8 +280,6 @@ def main():
     ap.add_argument("--no-fused-bwd", action="store_true",
                     help="64-output blocks: data-gradient GEMM + side-stream weight-gradient pass instead of "
                          "the fused block backward (A/B)")
-    ap.add_argument("--no-defer-reduce", action="store_true",
-                    help="fused block backward reduces its slabs on the main stream (A/B)")
     ap.add_argument("--fuse", choices=("auto", "always"), default="auto",
                     help="fused conv forward on the levels >= 64x64 (auto) or on every level (A/B)")
     ap.add_argument("--recompute-y128", action="store_true",
@@ -321,7 +319,6 @@ def main():
     model.engine.use_x3 = not args.no_x3
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
-    model.engine.defer_fused_reduce = not args.no_defer_reduce
     if args.recompute_y128:
         model.engine.recompute_y_couts = (64, 128)
     elif args.recompute_y64_128:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 11
+#define UNET_ABI_VERSION 10
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -220,13 +220,6 @@ int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float
  * head's gradient is rank one, da[m][c] = da_dlogit[m] * da_kernel[c] (unet_head_bwd_bnstats'
  * dlogit output and the head's 1x1 kernel, model/u_net.py:105-112), formed on load with the
  * same product the head would have stored (ABI 10).                                          */
-/* (ABI 11) d_dw_kernel = d_pw_kernel = NULL: the per-block slabs stay in ws and
- * unet_sepconv_bwd_reduce sums them later, e.g. on a second stream after an event, so the caller's
- * critical path does not wait for the two fixed-order slab reductions (ws must then stay untouched
- * until that call has run).                                                                   */
-int unet_sepconv_bwd_reduce(int n, int h, int w, int cin, int cout, const void* ws,
-                            size_t ws_bytes, float* d_dw_kernel, float* d_pw_kernel,
-                            unet_stream_t stream);
 int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                            const float* pw_kernel, const float* da, const float* da_dlogit,
                            const float* da_kernel, const float* z,

@@ -918,13 +918,6 @@ def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn):
         outs1.append((dy1, ddk1, dpk1))
     for x1, x2 in zip(*outs1):
         assert torch.equal(x1, x2)
-    # deferred slab reduction (ABI 11): the pass leaves its slabs, unet_sepconv_bwd_reduce sums them
-    slabs = torch.empty(ops.sepconv_bwd_workspace_numel(n, h, w, C, cout), device="cuda")
-    dy_d = torch.empty((n, h, w, C), device="cuda")
-    ops.sepconv_bwd_fused(v, n, h, w, dk, pk, tda, tz, ts, th, coef, cout, dy_d, None, None, slabs=slabs)
-    ddk_d, dpk_d = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
-    ops.sepconv_bwd_reduce(n, h, w, C, cout, slabs, ddk_d, dpk_d)
-    assert torch.equal(dy_d, dy_f) and torch.equal(ddk_d, ddk_f) and torch.equal(dpk_d, dpk_f)
     # float64 oracle
     if use_bn:
         rz, _, _ = K.bn_relu_bwd(da, z, gamma, beta, f32(mean), f32(var))

@@ -561,29 +561,12 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
             break;
     }
     UNET_CHECK_LAUNCH(op);
-    if (!d_dw_kernel && !d_pw_kernel) return 0;  // (the caller reduces the slabs later: unet_sepconv_bwd_reduce)
     const int64_t lp = (int64_t)cin * cout, ld = (int64_t)9 * cin;
     int rc = reduce_slabs(a.pw_slab, p.S, lp, d_pw_kernel, lp, lp, st);
     if (rc) return rc;
     return reduce_slabs(a.dw_slab, p.S, ld, d_dw_kernel, ld, ld, st);
 }
 }  // namespace
-
-extern "C" int unet_sepconv_bwd_reduce(int n, int h, int w, int cin, int cout, const void* ws, size_t ws_bytes,
-                                       float* d_dw_kernel, float* d_pw_kernel, unet_stream_t stream) {
-    const size_t need = unet_sepconv_bwd_filter_workspace(n, h, w, cin, cout);
-    UNET_CHECK_ARG(need && ws && ws_bytes >= need && d_dw_kernel && d_pw_kernel,
-                   "unet_sepconv_bwd_reduce: bad arguments (workspace %zu < %zu or null output)", ws_bytes, need);
-    const SwPlan p = sw_plan(n, h, w, cin);
-    float* pw_slab = static_cast<float*>(const_cast<void*>(ws));
-    float* dw_slab = reinterpret_cast<float*>(static_cast<char*>(const_cast<void*>(ws)) +
-                                              align_up((size_t)p.S * cin * cout * sizeof(float), 256));
-    hipStream_t st = as_stream(stream);
-    const int64_t lp = (int64_t)cin * cout, ld = (int64_t)9 * cin;
-    int rc = reduce_slabs(pw_slab, p.S, lp, d_pw_kernel, lp, lp, st);
-    if (rc) return rc;
-    return reduce_slabs(dw_slab, p.S, ld, d_dw_kernel, ld, ld, st);
-}
 
 extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
                                       const float* pw_kernel, const float* da, const float* da_dlogit,
@@ -595,9 +578,8 @@ extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, c
     UNET_CHECK_ARG(cout == 64 && unet_sepconv_bwd_filter_supported(x, n, h, w, cout) && x->drop_rate == 0.f,
                    "%s: unsupported (needs 64 output channels, input channels %% 64 == 0, no dropout on the input, "
                    "a PLAIN / BNRELU / CONCAT view, h %% 8 == 0, w %% 16 == 0)", op);
-    UNET_CHECK_ARG(dw_kernel && pw_kernel && z && scale && shift && coef && dy, "%s: null pointer", op);
-    UNET_CHECK_ARG((d_dw_kernel == nullptr) == (d_pw_kernel == nullptr),
-                   "%s: d_dw_kernel and d_pw_kernel go together (both NULL: slabs left in ws)", op);
+    UNET_CHECK_ARG(dw_kernel && pw_kernel && z && scale && shift && coef && dy && d_dw_kernel && d_pw_kernel,
+                   "%s: null pointer", op);
     UNET_CHECK_ARG(da ? !da_dlogit && !da_kernel : da_dlogit && da_kernel,
                    "%s: give da, or da_dlogit and da_kernel (rank-one da)", op);
     UNET_CHECK_ARG(((uintptr_t)da | (uintptr_t)da_kernel | (uintptr_t)z | (uintptr_t)dy | (uintptr_t)scale | (uintptr_t)shift |

@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 11
+ABI_VERSION = 10
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -67,7 +67,6 @@ SIGNATURES = {
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_int, P, P, P, c_size_t, P]),
-    "unet_sepconv_bwd_reduce": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_size_t, P, P, P]),
     "unet_sepconv_bwd_fused": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P,
                                        c_size_t, P]),
     "unet_sepconv_set_schedule": (c_int, [c_int]),

@@ -96,7 +96,6 @@ class BlockBufs:
     zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
     dlogit: Optional[torch.Tensor] = None  # last block, binary head: dL/dlogit per pixel (its da is rank one)
     da_rank1: bool = False  # this backward's da is dlogit (x) the head kernel, never materialised
-    swslab: Optional[torch.Tensor] = None  # fused block backward: its weight-gradient slabs (reduced on the side)
 
 
 @dataclass
@@ -192,9 +191,6 @@ class UNetEngine:
         # weight gradients from it; dz never stored) instead of the data-gradient GEMM + the
         # side-stream weight-gradient pass
         self.fuse_block_bwd = True
-        # ... and its two fixed-order slab reductions run on the side stream (the main stream goes on
-        # to the depthwise data gradient at once)
-        self.defer_fused_reduce = True
         self._pending_side = None
         self._pending_ready: Optional[str] = None
         self._ev = None  # created on first use (on the device)
@@ -566,25 +562,13 @@ class UNetEngine:
                                                     bb.y, dy, self._gwts(b)[1])
             elif fused_bwd:  # dy and both weight gradients in one pass over (da, z, the input view)
                 gdk_f, gpk_f = self._gwts(b)
-                cin = view_f.channels
-                # two streams: the pass leaves its per-block slabs and the side stream sums them, so
-                # the main stream goes straight on to the depthwise data gradient
-                slabs = None
-                if self.overlap and self.defer_fused_reduce:
-                    ns = ops.sepconv_bwd_workspace_numel(n, h, w, cin, b.cout)
-                    if bb.swslab is None or bb.swslab.numel() != ns:
-                        bb.swslab = torch.empty(ns, dtype=torch.float32, device=self.device)
-                    slabs = bb.swslab
-                gk = (None, None) if slabs is not None else (gdk_f, gpk_f)
                 if bb.da_rank1:  # the binary head's da = dlogit (x) kernel, formed on load
                     ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, None, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
-                                          dy, *gk, da_rank1=(bb.dlogit, self.vars["output_mask/kernel"]), slabs=slabs)
+                                          dy, gdk_f, gpk_f, da_rank1=(bb.dlogit, self.vars["output_mask/kernel"]))
                     bb.da_rank1 = False
                 else:
                     ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, bb.da, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
-                                          dy, *gk, slabs=slabs)
-                if slabs is not None:
-                    self.run_beside(lambda: ops.sepconv_bwd_reduce(n, h, w, cin, b.cout, slabs, gdk_f, gpk_f))
+                                          dy, gdk_f, gpk_f)
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, dz)

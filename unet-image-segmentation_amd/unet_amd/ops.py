@@ -402,14 +402,12 @@ def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> 
 
 
 def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, da: Optional[Tensor], z: Tensor,
-                      scale: Tensor, shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Optional[Tensor],
-                      dpk: Optional[Tensor], da_rank1: Optional[Tuple[Tensor, Tensor]] = None,
-                      slabs: Optional[Tensor] = None):
+                      scale: Tensor, shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Tensor, dpk: Tensor,
+                      da_rank1: Optional[Tuple[Tensor, Tensor]] = None):
     """A 64-output block's BN + ReLU backward, pointwise data gradient and both weight gradients
     in one pass (dz never stored): dy out, d_depthwise / d_pointwise kernels overwritten.
     da_rank1 = (dlogit (m,), head kernel (cout,)) instead of da: the binary head's rank-one
-    gradient, formed on load.  ddk = dpk = None: the weight gradients stay as per-block slabs in
-    `slabs` (sepconv_bwd_workspace_numel floats) for a later sepconv_bwd_reduce."""
+    gradient, formed on load."""
     C = x.channels
     m = n * h * w
     _check(dk, "depthwise_kernel", 9 * C)
@@ -426,36 +424,15 @@ def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, d
     _check(z, "z", m * cout)
     _check(coef, "coef", 3 * cout)
     _check(dy, "dy", m * C)
-    if (ddk is None) != (dpk is None) or (ddk is None and slabs is None):
-        raise ValueError("sepconv_bwd_fused: ddk and dpk go together; without them pass slabs")
-    if ddk is not None:
-        _check(ddk, "d_depthwise_kernel", 9 * C)
-        _check(dpk, "d_pointwise_kernel", C * cout)
-    if slabs is not None:
-        _check(slabs, "slabs", sepconv_bwd_workspace_numel(n, h, w, C, cout))
-        ws, wsb = _ptr(slabs), slabs.numel() * 4
-    else:
-        ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
+    _check(ddk, "d_depthwise_kernel", 9 * C)
+    _check(dpk, "d_pointwise_kernel", C * cout)
+    ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
     vs = x.c_struct()
     _call("unet_sepconv_bwd_fused", (4.0 * m * C * cout + 36.0 * m * C,
                                      x.src_bytes(n, h, w) + 4.0 * (m * C + m * cout) + da_bytes),
           ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(pk), _ptr(da), _ptr(da_rank1[0] if da_rank1 else None),
           _ptr(da_rank1[1] if da_rank1 else None), _ptr(z), _ptr(scale), _ptr(shift), _ptr(coef), cout,
           _ptr(dy), _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
-
-
-def sepconv_bwd_workspace_numel(n: int, h: int, w: int, cin: int, cout: int) -> int:
-    """floats of the per-block weight-gradient slabs of sepconv_bwd_fused / _filter"""
-    return (L.query("unet_sepconv_bwd_filter_workspace", n, h, w, cin, cout) + 3) // 4
-
-
-def sepconv_bwd_reduce(n: int, h: int, w: int, cin: int, cout: int, slabs: Tensor, ddk: Tensor, dpk: Tensor):
-    """The fixed-order sums of a deferred sepconv_bwd_fused's slabs into the two kernel gradients."""
-    _check(slabs, "slabs", sepconv_bwd_workspace_numel(n, h, w, cin, cout))
-    _check(ddk, "d_depthwise_kernel", 9 * cin)
-    _check(dpk, "d_pointwise_kernel", cin * cout)
-    _call("unet_sepconv_bwd_reduce", (0.0, 4.0 * slabs.numel()), n, h, w, cin, cout, _ptr(slabs),
-          slabs.numel() * 4, _ptr(ddk), _ptr(dpk), _stream())
 
 
 def sepconv_bwd_filter(x: View, n: int, h: int, w: int, dk: Tensor, dy: Tensor, dz: Tensor, cout: int,
