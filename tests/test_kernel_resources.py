@@ -1,0 +1,88 @@
+"""Register and scratch budget of the product library's gfx950 kernels, read from the code-object
+metadata embedded in libunet_hip.so (host only: no GPU).  A kernel that spills to scratch memory
+pays a global-memory round trip per spilled value; only the fused-forward kernels named below are
+allowed to, by the amounts DESIGN.md §8 records (the 256-column split tile at its two-wave
+256-register cap, the 64-column one at three waves)."""
+import os
+import re
+import shutil
+import struct
+import subprocess
+import tempfile
+from pathlib import Path
+
+import pytest
+
+LIB = Path(__file__).resolve().parents[1] / "unet-image-segmentation_amd" / "unet_amd" / "libunet_hip.so"
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _tool(name):
+    p = LLVM / name
+    return str(p) if p.exists() else shutil.which(name)
+
+
+def _kernel_resources():
+    """{kernel symbol: (scratch bytes per lane, spilled VGPRs)} over every gfx950 code object."""
+    objcopy, readelf = _tool("llvm-objcopy"), _tool("llvm-readelf")
+    if not (LIB.exists() and objcopy and readelf):
+        pytest.skip("needs the built libunet_hip.so and llvm-objcopy / llvm-readelf")
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", str(LIB)], check=True,
+                       capture_output=True)
+        blob = open(fat, "rb").read()
+        pos, k = 0, 0
+        while (i := blob.find(BUNDLE_MAGIC, pos)) >= 0:
+            (entries,) = struct.unpack_from("<Q", blob, i + 24)
+            p = i + 32
+            for _ in range(entries):
+                off, size, tlen = struct.unpack_from("<QQQ", blob, p)
+                triple = blob[p + 24:p + 24 + tlen].decode()
+                p += 24 + tlen
+                if "gfx950" not in triple or size == 0:
+                    continue
+                elf = os.path.join(d, f"co{k}.elf")
+                k += 1
+                open(elf, "wb").write(blob[i + off:i + off + size])
+                notes = subprocess.run([readelf, "--notes", elf], check=True, capture_output=True,
+                                       text=True).stdout
+                name = None
+                scratch = spills = 0
+                for line in notes.splitlines():
+                    m = re.match(r"\s+\.name:\s+(\S+)", line)
+                    if m:
+                        if name is not None:
+                            out[name] = (scratch, spills)
+                        name, scratch, spills = m.group(1), 0, 0
+                        continue
+                    m = re.match(r"\s+\.private_segment_fixed_size:\s+(\d+)", line)
+                    if m:
+                        scratch = int(m.group(1))
+                    m = re.match(r"\s+\.vgpr_spill_count:\s+(\d+)", line)
+                    if m:
+                        spills = int(m.group(1))
+                if name is not None:
+                    out[name] = (scratch, spills)
+            pos = i + len(BUNDLE_MAGIC)
+    assert k > 0, "no gfx950 code object in libunet_hip.so"
+    return out
+
+
+def test_only_fused_forward_kernels_use_scratch():
+    res = _kernel_resources()
+    assert len(res) > 100
+    allowed = re.compile(r"sepconv_(rk|fwd)_kernel")
+    offenders = {n: r for n, r in res.items() if r[0] > 0 and not allowed.search(n)}
+    assert not offenders, f"kernels spilling to scratch: {offenders}"
+
+
+def test_split_precision_128_column_tile_does_not_spill():
+    # sepconv_rk_kernel<MODE, DROP, EPI, BN = 128, WRITE_Y, X6 = true>: two waves per SIMD (its
+    # LDS allows two blocks per CU), so it fits in registers
+    res = _kernel_resources()
+    tiles = {n: r for n, r in res.items() if re.search(r"sepconv_rk_kernelILi\d+ELb[01]ELi\d+ELi128ELb[01]ELb1E", n)}
+    assert tiles, "no 128-column split-precision fused-forward kernels found"
+    assert all(r == (0, 0) for r in tiles.values()), tiles
