@@ -1,8 +1,8 @@
 """Register and scratch budget of the product library's gfx950 kernels, read from the code-object
 metadata embedded in libunet_hip.so (host only: no GPU).  A kernel that spills to scratch memory
-pays a global-memory round trip per spilled value; only the fused-forward kernels named below are
-allowed to, by the amounts DESIGN.md §8 records (the 256-column split tile at its two-wave
-256-register cap, the 64-column one at three waves)."""
+pays a global-memory round trip per spilled value.  Only LDS-A-tile fused-forward variants that
+the default step does not launch (dropout views of the 64-column tile, max-pool views) spill
+today; the register-A kernels the step runs must stay within their registers."""
 import os
 import re
 import shutil
@@ -71,18 +71,18 @@ def _kernel_resources():
     return out
 
 
-def test_only_fused_forward_kernels_use_scratch():
+def test_only_lds_a_tile_fused_forward_uses_scratch():
     res = _kernel_resources()
     assert len(res) > 100
-    allowed = re.compile(r"sepconv_(rk|fwd)_kernel")
+    allowed = re.compile(r"sepconv_fwd_kernel")
     offenders = {n: r for n, r in res.items() if r[0] > 0 and not allowed.search(n)}
     assert not offenders, f"kernels spilling to scratch: {offenders}"
 
 
-def test_split_precision_128_column_tile_does_not_spill():
-    # sepconv_rk_kernel<MODE, DROP, EPI, BN = 128, WRITE_Y, X6 = true>: two waves per SIMD (its
-    # LDS allows two blocks per CU), so it fits in registers
+def test_register_a_fused_forward_does_not_spill():
+    # every register-A fused forward (sepconv_rk_kernel, the one the step runs at >= 64^2), and in
+    # particular the split-precision 128-column tile at its three-wave register cap
     res = _kernel_resources()
-    tiles = {n: r for n, r in res.items() if re.search(r"sepconv_rk_kernelILi\d+ELb[01]ELi\d+ELi128ELb[01]ELb1E", n)}
-    assert tiles, "no 128-column split-precision fused-forward kernels found"
+    tiles = {n: r for n, r in res.items() if "sepconv_rk_kernel" in n}
+    assert any(re.search(r"ELi128ELb[01]ELb1E", n) for n in tiles), "no 128-column split-precision kernels"
     assert all(r == (0, 0) for r in tiles.values()), tiles

@@ -52,11 +52,8 @@ struct RkLds {
 // A operand (same taps, same fmaf order: y bitwise equal), splits them into three bf16 fragments
 // (common.h split4) and runs mfma_x6 against the pre-split weight planes (SepArgs::pkx) per 32-column
 // tile: 6 x 32 MFMA cycles per stage and tile instead of 8 x 64.
-// Waves per SIMD: three only for the 64-column split tile (42 KB of LDS, three blocks per CU);
-// the 128-column one holds 55 KB, i.e. two blocks per CU, so it gets two waves' registers (a
-// three-wave cap spilled 66-114 VGPRs to scratch for an occupancy the LDS never allowed).
 template <int MODE, bool DROP, int EPI, int BN, bool WRITE_Y, bool X6 = false>
-__global__ __launch_bounds__(256, X6 && BN <= 64 ? 3 : 2) void sepconv_rk_kernel(SepArgs g) {
+__global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kernel(SepArgs g) {
     static_assert(!X6 || MODE != UNET_VIEW_POOL_BNRELU, "X6: no max-pool views");
     constexpr int TN = BN / 32;                 // MFMA tiles per wave (all BN columns)
     constexpr int NH = HPIX * (BK / 4);         // halo float4 per stage (720)
