@@ -180,18 +180,26 @@ def encoder_block_roofline(batch, size, device, reps=10, x3=True):
 
 
 def pmc_traffic(op):
-    """HBM bytes per launch of `op` from the newest committed PMC summary (profiles/*_traffic.json,
-    written by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    """HBM bytes per launch of `op` from the committed PMC summary (profiles/*traffic*.json, written
+    by tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes of this bench) made for THIS library
+    build: the summary's lib_sha16 must equal the sha256 of the loaded libunet_hip.so.  Without
+    such a summary traffic is null and the source says why."""
     import glob
-    files = glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))
-    for f in sorted(files, key=lambda f: (os.path.getmtime(f), f), reverse=True):  # newest first
+    import hashlib
+    from unet_amd import _lib
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    except (OSError, AttributeError):
+        return None, "library hash unavailable"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("op") == op:
+        if d.get("op") == op and d.get("lib_sha16") == sha:
             return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
-    return None, None
+    return None, f"no PMC summary for this library build (lib sha256 {sha})"
 
 
 def workload_config(args):
@@ -376,6 +384,28 @@ def main():
         dt_roof = time.perf_counter() - t1
         ops.TIMER = None
 
+    # data parallel: a separate pass of K steps measuring the all-reduce time the step exposes on
+    # the main stream (from the end of the backward's launches to the last bucket's completion)
+    dp_info = None
+    if world > 1:
+        probe = []
+        model.dp_probe = probe
+        for _ in range(args.steps):
+            model.train_step(x, y)
+        torch.cuda.synchronize()
+        model.dp_probe = None
+        ex = sorted(a.elapsed_time(b) for a, b in probe)
+        t = torch.tensor([ex[len(ex) // 2]], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        bk = model.bucketer
+        dp_info = {"backend": dist.get_backend(), "collective": "all_reduce(sum) of the flat fp32 gradient buffer, "
+                   "bucketed, issued from the side stream as the backward completes each bucket",
+                   "allreduce_exposed_ms": round(float(t.item()), 4),
+                   "allreduce_exposed_definition": f"median over {args.steps} steps (max over ranks) of HIP-event time on "
+                                                   "the main stream from the end of the backward to the last bucket",
+                   "buckets": len(bk.buckets), "bucket_bytes": [4 * (hi - lo) for lo, hi in bk.buckets],
+                   "grad_bytes": 4 * int(model.engine.grads.numel())}
+
     out = None
     if rank == 0:
         imgs = world * args.batch * args.steps
@@ -407,6 +437,8 @@ def main():
                 out["roofline"]["timing"] = (f"separate pass of {args.steps} steps after the timed region "
                                              f"({dt_roof / args.steps * 1e3:.3f} ms/step with events)")
                 out["op_breakdown"] = breakdown[:8]
+        if dp_info is not None:
+            out["data_parallel"] = dp_info
         if model.mean_iou is not None:
             out["mean_io_u"] = round(model.mean_iou.result(), 6)
         if not args.no_roofline and world == 1 and args.encoder_batch > 0:

@@ -23,12 +23,15 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("global_batch", [4, 5])
-def test_dp_two_ranks_equal_weighted_single_process(global_batch):
+@pytest.mark.parametrize("global_batch,deferred", [(4, False), (5, False), (5, True)])
+def test_dp_two_ranks_equal_weighted_single_process(global_batch, deferred):
     """tools/dp_check.py: the DP step equals sum_r (n_r / n) x (single-process gradient of shard r)
-    through AdamW (equal shards 2+2 and unequal 3+2), and the ranks agree bitwise."""
+    through AdamW (equal shards 2+2 and unequal 3+2), and the ranks agree bitwise.  deferred: the
+    64-output blocks' weight gradients go to the deferred side-stream pass, so the bucketed
+    all-reduce's low-water reports wait for a pending deferral."""
     env = dict(os.environ)
     env["DP_CHECK_GLOBAL"] = str(global_batch)
+    env["DP_CHECK_DEFERRED"] = "1" if deferred else "0"
     if torch.cuda.device_count() < 2:
         env["UNET_DP_ONE_DEVICE"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -57,3 +60,8 @@ def test_bench_gpus_flag_spawns_ranks():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 32, out
     assert out["config"]["parallelism"] == "dp2"
+    dp = out["data_parallel"]  # the all-reduce exposure pass
+    assert dp["backend"] in ("nccl", "gloo") and dp["buckets"] >= 1 and dp["allreduce_exposed_ms"] >= 0
+    assert sum(dp["bucket_bytes"]) == dp["grad_bytes"]
+    if torch.cuda.device_count() >= 2:
+        assert dp["backend"] == "nccl"  # RCCL

@@ -201,6 +201,30 @@ def test_determinism_bitwise():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+def test_inplace_weight_edit_reaches_split_planes():
+    """the split-precision (bf16 x 3) pointwise planes the fused forward reads are
+    re-split on every forward, so an in-place write to engine.vars (a custom optimizer loop, a
+    broadcast) changes predict() exactly as set_weights_dict of the same values does."""
+    from unet_amd.model import UNetModel
+    rng = np.random.default_rng(21)
+    x, _ = _data(rng, 2, 64, 64, 1)
+    m = UNetModel((64, 64, 3), 1, dropout_rate=0.0, seed=3)
+    xd = torch.from_numpy(x).cuda()
+    p0 = m.engine.predict(xd)
+    name = "enc1_block2_sepconv/pointwise_kernel"  # a fused split-precision block (64 x 64 level)
+    assert "enc1_block2" in m.engine.x3_off
+    w = m.engine.vars[name]
+    new = (w * -1.5 + 0.01).contiguous()
+    w.copy_(new)  # in place: no set_weights_dict, no version bump
+    p1 = m.engine.predict(xd)
+    ref = UNetModel((64, 64, 3), 1, dropout_rate=0.0, seed=3)
+    ref.engine.set_weights_dict({name: new.cpu().numpy()})
+    p2 = ref.engine.predict(xd)
+    torch.cuda.synchronize()
+    assert not torch.equal(p0, p1)
+    assert torch.equal(p1, p2)
+
+
 def test_stream_schedules_bitwise_equal():
     """The schedule only orders launches: single-stream, two-stream with the weight gradients issued
     beside their data gradient, and two-stream with the fused 256x256-level weight gradient deferred

@@ -149,3 +149,28 @@ def test_train_sample_count_fallback(tmp_path, capsys):
     with pytest.raises(SystemExit) as e:
         count_samples(Bad(), Bad(), str(tmp_path / "missing"))
     assert e.value.code == 1
+
+
+def test_train_loader_error_banner(tmp_path, capsys):
+    """A missing dataset tree ends train.py the reference's way: the 'Error initializing
+    ImageDataGenerator' block closed by its dashed line, exit 1 (reference scripts/train.py:208-217).
+    No device work happens before the loaders are built."""
+    from scripts.train import main
+    with pytest.raises(SystemExit) as e:
+        main(["--dataset-root", str(tmp_path / "missing"), "--epochs", "1"])
+    out = capsys.readouterr().out
+    assert e.value.code == 1
+    assert "\n--- Error initializing ImageDataGenerator ---\n" in out
+    assert "-------------------------------------------\n" in out
+
+
+def test_train_stdout_strings_match_reference():
+    """The banner strings train.py prints around the training loop (reference
+    scripts/train.py:301, 333-338): the TensorBoard log line and the closing dashed line of the
+    training-error block."""
+    import inspect
+    import scripts.train as T
+    src = inspect.getsource(T.main)
+    assert 'TensorBoard logs will be saved to: {log_dir}' in src
+    i = src.index('print("\\n--- Error during model training ---")')
+    assert 'print("-----------------------------------\\n")' in src[i:]

@@ -34,7 +34,20 @@ HW, SEED, LR, WD = 64, 5, 2e-3, 1e-4
 x_all, y_all = synthetic_batch(G, HW, HW, 1, 77, dev)
 lo, hi = shard_bounds(G, world, rank)
 
-m = UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED)
+# DP_CHECK_DEFERRED=1: the 64-output blocks take the data-gradient GEMM + the deferred side-stream
+# weight-gradient pass (no fused block backward), so the all-reduce low-water reports meet a
+# pending deferral (engine._grads_ready / _flush_side)
+DEFERRED = os.environ.get("DP_CHECK_DEFERRED") == "1"
+
+
+def configure(model):
+    if DEFERRED:
+        model.engine.fuse_block_bwd = False
+        model.engine.defer_sw = True
+    return model
+
+
+m = configure(UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED))
 m.compile(AdamW(LR, WD), "dice_loss")
 m.enable_data_parallel(bucket_bytes=1 << 20)  # many buckets
 m.train_step(x_all[lo:hi], y_all[lo:hi], global_size=G)
@@ -49,7 +62,7 @@ exp_g = torch.zeros_like(g_dp, dtype=torch.float64)
 exp_s = torch.zeros_like(s_dp, dtype=torch.float64)
 for r in range(world):
     a, b = shard_bounds(G, world, r)
-    ref = UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED)
+    ref = configure(UNetModel((HW, HW, 3), 1, dropout_rate=0.2, device=dev, seed=SEED))
     ref.engine.rank_salt = r
     ref.compile(AdamW(LR, WD), "dice_loss")
     ref.train_step(x_all[a:b], y_all[a:b])

@@ -4,14 +4,30 @@ WRITE_SIZE, separate runs of the same bench command, kernel-trace only).
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE counts half the bytes of wide coalesced streaming reads, so it is doubled; WRITE_SIZE
 is exact for 16-B-per-lane stores.  Infinity-Cache hits are counted as fetches, so this is an
-upper bound on HBM bytes.
+upper bound on HBM bytes.  The summary records the sha256 (first 16 hex digits) of the library
+build it measured (`lib_sha16`); bench.py only quotes a summary whose hash matches the library
+it runs.
 
 usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [OP]
 """
 import csv
+import hashlib
 import json
+import os
 import re
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "unet-image-segmentation_amd",
+                   "unet_amd", "libunet_hip.so")
+
+
+def lib_sha16(path=LIB):
+    """sha256 of the library build, first 16 hex digits (None if it is not built)."""
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 # the kernels each C-ABI op launches (training-mode epilogues); the optional trailing flag is the
 # split-precision (X6) template parameter, false in the product library
@@ -43,7 +59,7 @@ def main():
     res = {"op": op, "kernel_regex": pat, "dispatches": [nf, nw],
            "fetch_bytes_per_launch_raw": round(f), "fetch_bytes_per_launch": round(2 * f),
            "write_bytes_per_launch": round(w), "traffic_bytes_per_launch": round(2 * f + w),
-           "sources": [fetch_csv, write_csv],
+           "sources": [fetch_csv, write_csv], "lib_sha16": lib_sha16(),
            "correction": "FETCH_SIZE x1024 x2 (gfx950 half-count of wide reads), WRITE_SIZE x1024"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))

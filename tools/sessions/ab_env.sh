@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/ab_env.sh N "VAR=a" "VAR=b" -- alternate two environment settings, N benches each
+# usage: tools/sessions/ab_env.sh N "VAR=a" "VAR=b" -- alternate two environment settings, N benches each
 source "$(dirname "$0")/gpu_session.sh"
 N=$1; shift
 for i in $(seq 1 "$N"); do

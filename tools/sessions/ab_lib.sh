@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/ab_lib.sh N -- alternate the in-tree library and libunet_hip_ab.so, N benches each
+# usage: tools/sessions/ab_lib.sh N -- alternate the in-tree library and libunet_hip_ab.so, N benches each
 source "$(dirname "$0")/gpu_session.sh"
 AB=unet-image-segmentation_amd/unet_amd/libunet_hip_ab.so
 for i in $(seq 1 "$1"); do

@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_ab_lib.sh ALT_SO -- bench A/B between the built libunet_hip.so and an alternative build
+# usage: tools/sessions/gpu_ab_lib.sh ALT_SO -- bench A/B between the built libunet_hip.so and an alternative build
 # of the same sources (e.g. a -D variant), swapping the file in place between runs (restored at the end).
 source "$(dirname "$0")/gpu_session.sh"
 L=unet-image-segmentation_amd/unet_amd

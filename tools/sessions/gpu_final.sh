@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_final.sh TAG -- round evidence: GPU tests, smoke, full bench (encoder blocks + CPU
+# usage: tools/sessions/gpu_final.sh TAG -- round evidence: GPU tests, smoke, full bench (encoder blocks + CPU
 # baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE / WRITE_SIZE passes.
 source "$(dirname "$0")/gpu_session.sh"
 TAG=${1:-run}

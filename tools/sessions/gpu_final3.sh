@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_final3.sh TAG -- round-3 evidence: GPU tests, smoke, full bench (encoder table + CPU
+# usage: tools/sessions/gpu_final3.sh TAG -- round-3 evidence: GPU tests, smoke, full bench (encoder table + CPU
 # baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE / WRITE_SIZE
 # passes of the bench, and a PMC group on enc2_block1's forward at batch 32
 source "$(dirname "$0")/gpu_session.sh"

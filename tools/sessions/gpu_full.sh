@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_full.sh TAG [gemm]  -- tests, bench, rocprof kernel stats (+ optional GEMM microbench)
+# usage: tools/sessions/gpu_full.sh TAG [gemm]  -- tests, bench, rocprof kernel stats (+ optional GEMM microbench)
 source "$(dirname "$0")/gpu_session.sh"
 TAG=${1:-run}
 run ops 600 python -m pytest tests/test_ops_gpu.py -q -x

@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_pmc_bench.sh TAG -- clean single-stream kernel trace + FETCH_SIZE / WRITE_SIZE
+# usage: tools/sessions/gpu_pmc_bench.sh TAG -- clean single-stream kernel trace + FETCH_SIZE / WRITE_SIZE
 # passes (separate runs, kernel-trace only) of a short bench.py run, for the roofline `traffic`.
 source "$(dirname "$0")/gpu_session.sh"
 TAG=${1:-run}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: tools/gpu_pmc_step.sh TAG -- bench line + FETCH_SIZE / WRITE_SIZE passes of a short bench run (whole-step traffic)
+# usage: tools/sessions/gpu_pmc_step.sh TAG -- bench line + FETCH_SIZE / WRITE_SIZE passes of a short bench run (whole-step traffic)
 source "$(dirname "$0")/gpu_session.sh"
 TAG=${1:-st}
 B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline --encoder-batch 0"

@@ -1,7 +1,7 @@
 #!/bin/bash
-# usage: tools/gpu_r2.sh TAG [steps...] -- round-3 GPU session: steps from {parity,tests,smoke,bench,prof,prof1s,pmc}
+# usage: tools/sessions/gpu_r2.sh TAG [steps...] -- round-2 GPU session: steps from {parity,tests,smoke,bench,prof,prof1s,pmc}
 source "$(dirname "$0")/gpu_session.sh"
-TAG=${1:-r3}; shift
+TAG=${1:-r2}; shift
 export UNET_PARITY_LOG=gpurun_out/parity_${TAG}.jsonl
 B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline --encoder-batch 0"
 for s in "$@"; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Runs GPU steps in order; each under its own time limit.  Test failures (exit 1) do not stop
 # the session; a crash, abort, fault or timeout does (no further GPU work after it).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 run() {  # run <name> <timeout> <cmd...>

@@ -148,7 +148,7 @@ def main(argv=None):
                              args.batch_size, SEED, shuffle=False, horizontal_flip=False, rank=rank, world=world)
         say("Data Generators created successfully.")
     except Exception as e:  # reference: print + exit(1) (train.py:208-217)
-        print("\n--- Error initializing data loaders ---")
+        print("\n--- Error initializing ImageDataGenerator ---")
         print(f"{e}")
         print("Please ensure dataset directories exist and follow the expected structure:")
         print(f"  Train Images: {TRAIN_FRAMES_DIR}/..")
@@ -199,7 +199,7 @@ def main(argv=None):
         callbacks.insert(0, ModelCheckpoint(filepath=args.model_out, monitor=monitor_metric, mode=monitor_mode,
                                             save_best_only=True, verbose=1))
         log_dir = os.path.join("./logs", time.strftime("%Y%m%d_%H%M%S"))
-        say(f"Logs will be saved to: {log_dir}")
+        say(f"TensorBoard logs will be saved to: {log_dir}")
         callbacks.append(JSONLogger(log_dir))
 
     say(f"\n--- Starting Training ({args.epochs} epochs) ---")
@@ -219,6 +219,7 @@ def main(argv=None):
         print(f"{e}")
         import traceback
         traceback.print_exc()
+        print("-----------------------------------\n")
         sys.exit(1)
 
 

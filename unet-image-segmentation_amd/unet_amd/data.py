@@ -20,11 +20,20 @@ engine weights its shard's loss gradient (model.train_step).
 from __future__ import annotations
 
 import os
+import threading
 from typing import Iterator, Tuple
 
 import numpy as np
 
 from .dp import shard_bounds
+
+
+def local_world_size() -> int:
+    """Data-parallel ranks on this host (torchrun's LOCAL_WORLD_SIZE; 1 without a launcher)."""
+    try:
+        return max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    except ValueError:
+        return 1
 
 
 class Shard(tuple):
@@ -71,12 +80,13 @@ def load_image(path, size, mode):
 
 class PairLoader:
     """cache_bytes: decoded, resized samples are kept as uint8 (256 x 256 x 4 B = 256 KiB per
-    pair at 256 x 256) up to this budget, so PNG decoding (~25 ms per 960 x 540 frame on one
+    pair at 256 x 256) up to this budget (default 8 GiB divided among this host's data-parallel
+    ranks, so a train + val loader pair on every rank of a node holds at most 16 GiB), so PNG decoding (~25 ms per 960 x 540 frame on one
     core, tools/bench_loader.py) is paid once per file, not once per epoch: the decode and resize
     are deterministic, so the batches are identical to decoding every epoch."""
 
     def __init__(self, frames_dir, masks_dir, size, batch_size, seed, shuffle=True, horizontal_flip=False, rank=0,
-                 world=1, workers=16, cache_bytes=16 << 30):
+                 world=1, workers=16, cache_bytes=None):
         if batch_size < world:
             raise ValueError(f"batch size {batch_size} < {world} data-parallel ranks: every rank needs a sample")
         self.frames = [os.path.join(frames_dir, f) for f in _list(frames_dir)]
@@ -88,9 +98,12 @@ class PairLoader:
         self.samples = len(self.frames)
         self.workers = max(1, int(workers))
         self._pool = None
+        if cache_bytes is None:  # host-wide: 8 GiB per loader (train + val) shared by this node's ranks
+            cache_bytes = (8 << 30) // local_world_size()
         self.cache_bytes = int(cache_bytes)
         self._cache = {}
         self._cached_bytes = 0
+        self._lock = threading.Lock()
 
     def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
         epoch = 0
@@ -109,9 +122,10 @@ class PairLoader:
         if xy is None:
             xy = (load_image_u8(self.frames[i], self.size, "rgb"), load_image_u8(self.masks[i], self.size, "grayscale"))
             nb = xy[0].nbytes + xy[1].nbytes
-            if self._cached_bytes + nb <= self.cache_bytes:
-                self._cache[i] = xy  # (dict item assignment is atomic under the GIL)
-                self._cached_bytes += nb
+            with self._lock:  # decode threads share the budget: check-and-add as one step
+                if i not in self._cache and self._cached_bytes + nb <= self.cache_bytes:
+                    self._cache[i] = xy
+                    self._cached_bytes += nb
         x = xy[0].astype(np.float32) / 255.0  # rescale=1/255 (reference scripts/train.py:170-178)
         y = xy[1].astype(np.float32) / 255.0
         if flip:

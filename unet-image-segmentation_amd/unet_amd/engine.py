@@ -148,7 +148,7 @@ class UNetEngine:
             else:
                 o = self.stat_layout.offsets[s.name]
                 self.vars[s.name] = self.stats[o:o + s.size].view(s.shape)
-        self.params_version = 0  # bumped whenever the trainable weights change (split planes go stale)
+        self.params_version = 0  # bumped whenever the trainable weights are replaced (set_weights / train_step)
         self.set_weights_dict(init_weights(self.specs, self.seed))
         self._build_plan()
         self._build_x3()
@@ -224,12 +224,13 @@ class UNetEngine:
                 off += (3 * b.cin * b.cout + 7) // 8 * 8
         self.x3_segs = segs
         self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
-        self._x3_version = -1
 
     def _refresh_x3(self):
-        if self.use_x3 and self.x3_segs and self._x3_version != self.params_version:
+        """Re-split on EVERY forward (one small launch): the planes then always match the fp32
+        weights the backward reads, whatever wrote engine.params in between (AdamW, a custom
+        optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast)."""
+        if self.use_x3 and self.x3_segs:
             ops.split_x3(self.params, self.x3_segs, self.pkx)
-            self._x3_version = self.params_version
 
     def _pkx(self, b: "Block"):
         o = self.x3_off.get(b.name) if self.use_x3 else None
@@ -498,7 +499,11 @@ class UNetEngine:
         for them (_flush_side), so no bucket is reduced before its last writer is issued."""
         if self.grad_hook is not None:
             if self._pending_side is not None:
-                self._pending_ready = name  # the lowest offset reported so far wins
+                # keep the LOWEST flat offset reported while the deferral is pending (reports
+                # arrive in descending-offset order today, but the hook must not depend on it)
+                off = self.train_layout.offsets
+                if self._pending_ready is None or off[name] < off[self._pending_ready]:
+                    self._pending_ready = name
                 return
             if self.overlap:
                 self._side_wait_main()

@@ -48,6 +48,8 @@ class UNetModel:
         self.metric_names: List[str] = []
         self.mean_iou: Optional[MeanIoU] = None
         self.bucketer: Optional[GradBucketer] = None
+        # bench.py: a list collecting (end of backward, all-reduce done) HIP event pairs per step
+        self.dp_probe: Optional[list] = None
         self.stop_training = False
 
     # --------------------------------------------------------------------- keras API ---
@@ -108,7 +110,15 @@ class UNetModel:
                 res = res.clone()
                 res[0] = 1.0 - res[2]
             self.engine.backward(y, self.loss_kind, loss_scale)
+            probe = self.dp_probe
+            if probe is not None:  # bench.py's all-reduce exposure pass: main stream, end of backward
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(main)
             scale = self.bucketer.finish() if self.bucketer is not None else 1.0
+            if probe is not None:  # ... and once every bucket's all-reduce has completed on it
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(main)
+                probe.append((e0, e1))
             self.optimizer.apply(self.engine.params, self.engine.grads, scale)
             self.engine.params_version += 1
         caller.wait_stream(main)
