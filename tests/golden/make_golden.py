@@ -263,13 +263,19 @@ def train256c21_fixture():
     return train_big_fixture(256, 8, 21, 61, 12)
 
 
+def train512_fixture():
+    """configs[3] per GPU: 512x512x3 binary, batch 8 (the HBM-bound regime BASELINE.json names)."""
+    return train_big_fixture(512, 8, 1, 71, 13)
+
+
 def write(name, d):
     np.savez_compressed(os.path.join(HERE, name), **{k.replace("/", "|"): v for k, v in d.items()})
 
 
 BIG = {"fwd256.npz": fwd256_fixture, "fwd512.npz": fwd512_fixture, "fwd21.npz": fwd21_fixture,
        "samples.npz": samples_fixture, "train128.npz": train128_fixture, "train256.npz": train256_fixture,
-       "train256c21.npz": train256c21_fixture}
+       "train256c21.npz": train256c21_fixture,
+       "train512.npz": train512_fixture}
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:  # regenerate only the named fixtures

@@ -40,7 +40,7 @@ def test_oracle_reproduces_train_golden():
         assert np.allclose(new[k], v, rtol=1e-9, atol=1e-15), k
 
 
-SLOW = ("train256.npz", "train256c21.npz")  # ~4 min of float64 oracle each: checked below instead
+SLOW = ("train256.npz", "train256c21.npz", "train512.npz")  # 4-10 min of float64 oracle each: checked below
 
 
 @pytest.mark.parametrize("name", sorted(set(MG.BIG) - set(SLOW)))

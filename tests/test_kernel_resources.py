@@ -86,3 +86,13 @@ def test_register_a_fused_forward_does_not_spill():
     tiles = {n: r for n, r in res.items() if "sepconv_rk_kernel" in n}
     assert any(re.search(r"ELi128ELb[01]ELb1E", n) for n in tiles), "no 128-column split-precision kernels"
     assert all(r == (0, 0) for r in tiles.values()), tiles
+
+
+def test_persistent_fused_forward_keeps_its_staging_in_registers():
+    # the persistent split-precision forward (sepconv_px_kernel) holds two register sets of staged
+    # loads; a private array in scratch would put vmcnt(0) waits into its k-loop and drain the
+    # prefetch (round 4: a [2][3] uint4 array did exactly that)
+    res = _kernel_resources()
+    px = {n: r for n, r in res.items() if "sepconv_px_kernel" in n}
+    assert len(px) >= 48, len(px)
+    assert all(r == (0, 0) for r in px.values()), {n: r for n, r in px.items() if r != (0, 0)}

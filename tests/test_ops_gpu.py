@@ -864,6 +864,67 @@ def test_fused_sepconv_split_precision(ops, mode, n, h, w, c0, c1, cout, drop):
     assert rel_err(host(outs["x6"][2]), host(outs["f32"][2])) < 1e-5
 
 
+PX_CASES = [
+    # mode, n, h, w, c0, c1, cout, drop, train, zsel
+    (1, 2, 8, 16, 64, 0, 128, 0.0, True, True),       # one tile per block
+    (1, 3, 64, 96, 64, 0, 128, 0.0, True, False),     # several tiles per block (enc2_block1's shape)
+    (1, 7, 88, 208, 128, 0, 128, 0.0, True, True),    # 1001 tiles: runs of 1 and 2 tiles per block
+    (3, 2, 32, 64, 64, 64, 64, 0.2, True, False),     # concat + dropout (dec1_block1)
+    (3, 1, 16, 32, 64, 64, 128, 0.0, True, False),    # concat, 128 outputs
+    (0, 2, 64, 64, 128, 0, 64, 0.0, False, True),     # plain view, 128 -> 64, inference epilogue
+    (1, 4, 128, 128, 128, 0, 128, 0.0, True, True),   # enc2_block2's shape at batch 4
+    (3, 2, 256, 256, 64, 64, 64, 0.0, True, False),   # dec1_block1's shape at batch 2
+    (1, 2, 256, 256, 64, 0, 64, 0.0, True, True),     # enc1_block2 (64 -> 64: the one-tile kernel in both)
+]
+
+
+@pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop,train,zsel", PX_CASES)
+def test_sepconv_persistent_matches_one_tile(ops, mode, n, h, w, c0, c1, cout, drop, train, zsel):
+    """The persistent split-precision forward (sepconv_px.hip, schedule AUTO / RK) against the
+    one-tile-per-block register-A kernel (schedule RK1) with the same split planes: the same
+    products in the same order, so z, y and the pooling selection are bitwise equal; the per-tile
+    BN partials combine the four waves' 32-row moments by Chan's formula instead of a two-pass sum
+    over 128 rows (fp32 rounding apart).  Also against the float64 oracle."""
+    rng = np.random.default_rng(900 + mode + n + cout)
+    a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
+    C = c0 + c1
+    dk = dev(f32(rng.standard_normal((3, 3, C, 1))))
+    pk32 = f32(rng.standard_normal((1, 1, C, cout)) / np.sqrt(C))
+    pk = dev(pk32)
+    pkx = torch.empty(3 * C * cout, dtype=torch.int16, device="cuda")
+    ops.split_x3(pk, [(0, C, cout, 0)], pkx)
+    gamma = dev(f32(rng.standard_normal(cout))) if zsel else None
+    v = _mk_view(ops, mode, t, drop, 31)
+    m = n * h * w
+    outs = []
+    for sch in (ops.SEPCONV_RK1, ops.SEPCONV_AUTO):
+        old = ops.sepconv_set_schedule(sch)
+        try:
+            y = torch.full((n, h, w, C), -7.0, device="cuda") if train else None
+            z = torch.full((n, h, w, cout), float("nan"), device="cuda")
+            part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda") if train else None
+            zs = torch.full((n, h // 2, w // 2, cout), float("nan"), device="cuda") if zsel else None
+            ops.sepconv_fwd(v, n, h, w, dk, cout, pk, y, z, part, zs, gamma, pkx=pkx)
+            torch.cuda.synchronize()
+            outs.append([None if q is None else q.cpu() for q in (y, z, part, zs)])
+        finally:
+            ops.sepconv_set_schedule(old)
+    (y1, z1, p1, s1), (y2, z2, p2, s2) = outs
+    assert torch.equal(z1, z2)
+    if train:
+        assert torch.equal(y1, y2)
+        nb = m // 128 * cout * 2
+        pa, pb = p1[:nb].view(-1, cout, 2).double(), p2[:nb].view(-1, cout, 2).double()
+        assert float((pa[..., 0] - pb[..., 0]).abs().max()) <= 1e-6 * float(pa[..., 0].abs().max() + 1)
+        assert rel_err(pb[..., 1].numpy(), pa[..., 1].numpy()) < 1e-5
+    if zsel:
+        assert torch.equal(s1, s2)
+    if m <= 64 * 1024:
+        xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"), drop, 31)
+        zr = K.pointwise(K.depthwise3x3(xv, host(dk)), pk32)
+        assert rel_err(z2.numpy(), zr) < 5e-6
+
+
 @pytest.mark.parametrize("mode,n,h,w,c0,c1", [(1, 2, 8, 16, 64, 0), (1, 1, 16, 32, 64, 0), (3, 1, 8, 32, 64, 64),
                                               (0, 2, 16, 16, 128, 0)])
 @pytest.mark.parametrize("use_bn", [True, False])

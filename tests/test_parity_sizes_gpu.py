@@ -197,9 +197,10 @@ def test_train_step_128_batch4():
             assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name
 
 
-@pytest.mark.parametrize("fixture,recompute128", [("train256.npz", False), ("train256c21.npz", False),
-                                                  ("train256.npz", True)])
-def test_train_step_training_geometry(fixture, recompute128):
+@pytest.mark.parametrize("fixture,recompute128,x3", [("train256.npz", False, True), ("train256c21.npz", False, True),
+                                                     ("train256.npz", True, True), ("train512.npz", False, True),
+                                                     ("train256c21.npz", False, False)])
+def test_train_step_training_geometry(fixture, recompute128, x3):
     """One train step at the geometry the reference trains at (scripts/train.py:84-88, 256x256)
     with configs[1]'s batch of 16 (binary) and configs[4]'s per-GPU batch of 8 (21 classes),
     against the committed float64 oracle step (tests/golden/make_golden.py train_big_fixture; the
@@ -217,6 +218,7 @@ def test_train_step_training_geometry(fixture, recompute128):
     g = _load(fixture)
     size, n, ncls = int(g["size"]), int(g["n"]), int(g["ncls"])
     m = UNetModel((size, size, 3), ncls, dropout_rate=0.0)
+    m.engine.use_x3 = x3  # False: the fp32-MFMA fused forward (the split-precision A/B)
     if recompute128:  # the 128-output blocks keep no y either: unet_sepconv_bwd_filter recomputes it
         m.engine.recompute_y_couts = (64, 128)
     w = MG.model_weights(ncls, MG.FULL, int(g["w_seed"]))
@@ -251,12 +253,16 @@ def test_train_step_training_geometry(fixture, recompute128):
         if e > lim:
             bad[k] = (e, lim)
     worst = sorted(errs.items(), key=lambda r: -r[1])[:5]
+    # each tensor's error against the float32 oracle's own distance to float64 on the same subsample
+    ratios = {k: errs[k] / max(float(g["e32sub:" + k]), 1e-30) for k in errs}
+    worst_ratio = sorted(ratios.items(), key=lambda r: -r[1])[:3]
     near0 = 0  # device pre-activations within fp32 rounding of the ReLU boundary (flip candidates)
     for b in m.engine.blocks:
         bb = A.blocks[b.name]
         pre = bb.z.double() * bb.scale.double() + bb.shift.double()
         near0 += int((pre.abs() < 1e-6 * (bb.shift.double().abs().max() + 1)).sum())
-    _log({"test": fixture, "loss": float(res[0]), "loss_ref": float(g["loss"]), "dice": float(res[1]),
+    _log({"test": fixture, "x3": x3, "recompute128": recompute128, "worst_ratio_to_e32sub": worst_ratio,
+          "loss": float(res[0]), "loss_ref": float(g["loss"]), "dice": float(res[1]),
           "bn_stats_worst_rel": bn_worst, "max_grad_rel_l2_sub": worst[0][1], "worst_grads": worst,
           "max_fp32_oracle_rel_l2": max(float(g["e32:" + k]) for k in grads), "relu_near_ties": near0})
     assert abs(res[0] - g["loss"]) < 1e-5 and abs(res[1] - g["dice"]) < 1e-5

@@ -11,6 +11,8 @@ mode, h, w, C, cout = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
 opt = sys.argv[7] if len(sys.argv) > 7 else ""
 N = int(os.environ.get("N", 16))
+if os.environ.get("SCHED"):  # 3 = RK1 (one tile per block), 0 = AUTO (persistent where it applies)
+    ops.sepconv_set_schedule(int(os.environ["SCHED"]))
 big = 2 if mode == 2 else 1
 src = torch.randn(N, big * h, big * w, C, device="cuda")
 sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1

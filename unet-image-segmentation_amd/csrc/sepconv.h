@@ -38,6 +38,10 @@ __device__ __forceinline__ float pool_sel(float a, float b, float c, float d, bo
 int launch_rk(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);
 bool rk_x6_supported(int mode, int cin);
 bool rk_supported(int mode, int cin, int cout);
+// persistent split-precision schedule (sepconv_px.hip) for 64 / 128 input and output channels:
+// returns 0, or -1 if the shape has no such kernel (needs a.pkx)
+bool px_supported(const SepArgs& a, int mode);
+int launch_px(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);
 
 }  // namespace sep
 }  // namespace unet

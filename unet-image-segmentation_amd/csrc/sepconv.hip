@@ -377,7 +377,7 @@ int g_sep_schedule = UNET_SEPCONV_AUTO;
 }
 
 extern "C" int unet_sepconv_set_schedule(int schedule) {
-    UNET_CHECK_ARG(schedule >= UNET_SEPCONV_AUTO && schedule <= UNET_SEPCONV_RK, "unet_sepconv_set_schedule: bad value");
+    UNET_CHECK_ARG(schedule >= UNET_SEPCONV_AUTO && schedule <= UNET_SEPCONV_RK1, "unet_sepconv_set_schedule: bad value");
     const int old = g_sep_schedule;
     g_sep_schedule = schedule;
     return old;
@@ -472,6 +472,13 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     // is forced; wider max-pool views keep the LDS-A-tile kernel (its 256-wide 8-wave tile pools
     // each halo element once for all columns)
     if (g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout)) {
+        // the persistent split-precision kernel for the short-K shapes (sepconv_px.hip), unless
+        // the one-tile-per-block register-A kernel is forced
+        if (g_sep_schedule != UNET_SEPCONV_RK1 && px_supported(a, x->mode)) {
+            if (launch_px(a, x->mode, drop, stats, wy, st)) return -1;
+            UNET_CHECK_LAUNCH("unet_sepconv_fwd");
+            return 0;
+        }
         if (launch_rk(a, x->mode, drop, stats, wy, st)) return -1;
         UNET_CHECK_LAUNCH("unet_sepconv_fwd");
         return 0;

@@ -326,7 +326,7 @@ def pointwise_bwd_filter(y: Tensor, dz: Tensor, m, cin, cout, dpk: Tensor):
           _ptr(dz), m, cin, cout, _ptr(dpk), ws, wsb, _stream())
 
 
-SEPCONV_AUTO, SEPCONV_TILE, SEPCONV_RK = 0, 1, 2
+SEPCONV_AUTO, SEPCONV_TILE, SEPCONV_RK, SEPCONV_RK1 = 0, 1, 2, 3
 
 
 def sepconv_set_schedule(schedule: int) -> int:
