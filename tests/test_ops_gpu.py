@@ -373,6 +373,38 @@ def test_head_dice(ops, ncls, loss_kind):
         ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, loss_kind, dx, dk, db, loss_scale=0.0)
 
 
+@pytest.mark.parametrize("ncls", [2, 3, 8, 21, 32])
+@pytest.mark.parametrize("cin,mode,nhw", [(64, 1, (3, 64, 40)), (16, 0, (2, 13, 11)), (48, 1, (1, 17, 19)),
+                                          (128, 1, (1, 9, 7)), (4, 1, (1, 300, 1))])
+def test_head_multiclass_shapes(ops, ncls, cin, mode, nhw):
+    """Softmax head forward + dice-loss backward (u_net.py:105-112, losses) over class counts that
+    round up to every register width (4..32), ragged and multi-tile pixel counts, the register
+    kernels (Cin <= 64, Cin/4 dividing 256) and the general ones (Cin 48 backward, Cin 128)."""
+    n, h, w = nhw
+    rng = np.random.default_rng(ncls * 131 + cin)
+    a, t = _view_inputs(rng, mode, n, h, w, cin)
+    v = _mk_view(ops, mode, t)
+    xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"))
+    k = f32(rng.standard_normal((1, 1, cin, ncls)) * 0.2)
+    b = f32(rng.standard_normal(ncls) * 0.1)
+    prob = torch.full((n, h, w, ncls), -1.0, device="cuda")
+    ops.head_fwd(v, n, h, w, ncls, dev(k), dev(b), prob)
+    pp = host(prob)
+    assert rel_err(pp, K.head(xv, k, b, ncls)) < 2e-6
+    yt = np.eye(ncls)[rng.integers(0, ncls, (n, h, w))]
+    sums = torch.empty(n * ncls * 3, device="cuda")
+    res = torch.empty(3, device="cuda")
+    ops.dice_fwd(dev(yt), prob, n, h * w, ncls, 1e-7, sums, res)
+    dx = torch.full((n, h, w, cin), 7.0, device="cuda")
+    dk = torch.empty((1, 1, cin, ncls), device="cuda")
+    db = torch.empty(ncls, device="cuda")
+    ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, 0, dx, dk, db)
+    rdx, rdk, rdb = K.head_bwd(xv, k, pp, K.dice_loss_grad(yt, pp), ncls)
+    assert rel_err(host(dx), rdx) < 1e-4
+    assert rel_err(host(dk), rdk) < 1e-4
+    assert rel_err(host(db), rdb) < 1e-4
+
+
 @pytest.mark.parametrize("ncls,thr", [(2, None), (2, 0.5), (5, None), (3, 0.3)])
 def test_meaniou(ops, ncls, thr):
     rng = np.random.default_rng(ncls)
@@ -388,6 +420,11 @@ def test_meaniou(ops, ncls, thr):
     ops.meaniou_update(dev(yt), dev(yp), ncls, thr, conf)
     ops.meaniou_update(dev(yt), dev(yp), ncls, thr, conf)  # accumulates
     ref = 2 * K.meaniou_confusion(f32(yt), f32(yp), ncls, thr)
+    assert np.array_equal(conf.cpu().numpy().reshape(ncls, ncls), ref)
+    # buffers not 16-byte aligned take the scalar kernel
+    conf.zero_()
+    ops.meaniou_update(dev(yt)[1:], dev(yp)[1:], ncls, thr, conf)
+    ref = K.meaniou_confusion(f32(yt)[1:], f32(yp)[1:], ncls, thr)
     assert np.array_equal(conf.cpu().numpy().reshape(ncls, ncls), ref)
 
 
@@ -685,46 +722,56 @@ def test_dwconv_bwd_data_bnstats(ops, mode, use_bn, n, h, w, c):
 
 @pytest.mark.parametrize("use_bn", [True, False])
 @pytest.mark.parametrize("loss_kind", [0, 1])
-def test_head_bwd_bnstats(ops, use_bn, loss_kind):
-    """Binary head backward that also emits the last block's BN-backward partials: dx / dW / db
-    bitwise equal to unet_head_bwd, statistics equal to unet_bn_relu_bwd_stats's."""
-    rng = np.random.default_rng(11 + loss_kind)
-    n, h, w, c = 2, 16, 24, 64
+@pytest.mark.parametrize("ncls,nhw", [(1, (2, 16, 24)), (21, (2, 16, 24)), (5, (1, 37, 41))])
+def test_head_bwd_bnstats(ops, use_bn, loss_kind, ncls, nhw):
+    """Head backward that also emits the last block's BN-backward partials (binary, and the fused
+    multi-class kernel): dx / dW / db bitwise equal to unet_head_bwd, statistics equal to
+    unet_bn_relu_bwd_stats's."""
+    rng = np.random.default_rng(11 + loss_kind + ncls)
+    n, h, w = nhw
+    c = 64
     a, t = _view_inputs(rng, 1, n, h, w, c)
     v = _mk_view(ops, 1, t)
-    k = dev(f32(rng.standard_normal((1, 1, c, 1)) * 0.2))
-    prob = dev(f32(rng.random((n, h, w, 1)) * 0.9 + 0.05))
-    yt = dev((rng.random((n, h, w, 1)) > 0.6).astype(np.float32))
-    sums = torch.empty(n * 3, device="cuda")
+    k = dev(f32(rng.standard_normal((1, 1, c, ncls)) * 0.2))
+    if ncls == 1:
+        prob = dev(f32(rng.random((n, h, w, 1)) * 0.9 + 0.05))
+        yt = dev((rng.random((n, h, w, 1)) > 0.6).astype(np.float32))
+    else:
+        lg = rng.standard_normal((n, h, w, ncls))
+        prob = dev(f32(np.exp(lg) / np.exp(lg).sum(-1, keepdims=True)))
+        yt = dev(f32(np.eye(ncls)[rng.integers(0, ncls, (n, h, w))]))
+    sums = torch.empty(n * ncls * 3, device="cuda")
     res = torch.empty(3, device="cuda")
-    ops.dice_fwd(yt, prob, n, h * w, 1, 1e-7, sums, res)
-    S = ops.head_bwd_bnstats_slabs(v, n, h, w, 1)
+    ops.dice_fwd(yt, prob, n, h * w, ncls, 1e-7, sums, res)
+    S = ops.head_bwd_bnstats_slabs(v, n, h, w, ncls)
     assert S > 0
     mean = dev(f32(rng.standard_normal(c) * 0.1))
     rstd = dev(f32(1.0 + rng.random(c)))
     part = torch.zeros(ops.bn_stats_partials_numel(S, c), device="cuda")  # counters zero
     outs = []
     for fused in (True, False):
-        dx, dk, db = torch.empty((n, h, w, c), device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
+        dx, dk, db = (torch.empty((n, h, w, c), device="cuda"), torch.empty(c * ncls, device="cuda"),
+                      torch.empty(ncls, device="cuda"))
         if fused:
-            ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db,
+            ops.head_bwd_bnstats(v, n, h, w, ncls, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db,
                                  mean if use_bn else None, rstd if use_bn else None, part)
         else:
-            ops.head_bwd(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db)
+            ops.head_bwd(v, n, h, w, ncls, k, prob, yt, sums, 1e-7, loss_kind, dx, dk, db)
         outs.append((dx, dk, db))
     for x, y in zip(outs[0], outs[1]):
         assert torch.equal(x, y)
-    # rank-one form (ABI 10): only dL/dlogit per pixel goes out; dx == dlogit (x) kernel bitwise,
-    # the same weight / bias gradients and BN-backward partials
-    dl, dk1, db1 = torch.empty(n * h * w, device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
-    part1 = torch.zeros_like(part)
-    ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1,
-                         mean if use_bn else None, rstd if use_bn else None, part1, dlogit=dl)
-    assert torch.equal(dl[:, None] * k.reshape(1, c), outs[0][0].reshape(-1, c))
-    assert torch.equal(dk1, outs[0][1]) and torch.equal(db1, outs[0][2])
-    assert torch.equal(part1, part)
-    with pytest.raises(ValueError):  # neither dx nor dlogit
-        ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1, None, None, part1)
+    if ncls == 1:
+        # rank-one form (ABI 10): only dL/dlogit per pixel goes out; dx == dlogit (x) kernel bitwise,
+        # the same weight / bias gradients and BN-backward partials
+        dl, dk1, db1 = torch.empty(n * h * w, device="cuda"), torch.empty(c, device="cuda"), torch.empty(1, device="cuda")
+        part1 = torch.zeros_like(part)
+        ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1,
+                             mean if use_bn else None, rstd if use_bn else None, part1, dlogit=dl)
+        assert torch.equal(dl[:, None] * k.reshape(1, c), outs[0][0].reshape(-1, c))
+        assert torch.equal(dk1, outs[0][1]) and torch.equal(db1, outs[0][2])
+        assert torch.equal(part1, part)
+        with pytest.raises(ValueError):  # neither dx nor dlogit
+            ops.head_bwd_bnstats(v, n, h, w, 1, k, prob, yt, sums, 1e-7, loss_kind, None, dk1, db1, None, None, part1)
     m = n * h * w
     st = []
     for fused in (True, False):

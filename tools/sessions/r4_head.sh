@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4: multi-class head rewrite -- op tests, 21-class model/parity tests, configs[4] b8 bench
+# with its kernel trace, configs[1] bench beside it
+source "$(dirname "$0")/gpu_session.sh"
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+run ops 300 $T tests/test_ops_gpu.py -k "head or meaniou or dice"
+run model 400 $T tests/test_model_gpu.py tests/test_parity_sizes_gpu.py -k "21 or c21 or multiclass or ncls"
+B4="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline --num-classes 21 --batch 8"
+run c4 200 $B4
+run c4tr 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c4 -o c4 -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline --encoder-batch 0 --num-classes 21 --batch 8
+run c1 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline

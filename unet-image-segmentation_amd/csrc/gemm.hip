@@ -58,7 +58,13 @@ struct RowsArgs {
     float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
     const float *bsc, *bsh, *bmu, *brs;  // E_BNPART: per-column BN scale/shift, mean/rstd (NULL: no xhat)
     float* bnpart;                       // E_BNPART: [cdiv(M, 128)][2][N] partial sums
+    int ko;  // lab build only (UNET_ROWS_KO): knock-out bits for timing decompositions, else 0
 };
+#ifdef UNET_LAB_BUILD
+#define ROWS_KO(g, bit) (((g).ko & (bit)) != 0)
+#else
+#define ROWS_KO(g, bit) false
+#endif
 
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
@@ -544,6 +550,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     auto load_stage = [&](int k0) {
         const int k = k0 + 4 * kq;
         ak = k;
+        if (k0 > 0 && ROWS_KO(g, 4)) return;  // lab: no k-loop operand loads
         const int kc = k < K ? k : 0;
         int koff = kc;
         if constexpr (AMODE == A_UNSHUFFLE) {
@@ -596,7 +603,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             }
             if (!kv || aoff[r] < 0) v = f4(0.f);
             if constexpr (AMODE == A_BNBWD) {
-                if (g.side && nt == 0 && kv && aoff[r] >= 0) st4(g.side + aoff[r] + ak, v);
+                if (g.side && nt == 0 && kv && aoff[r] >= 0 && !ROWS_KO(g, 2)) st4(g.side + aoff[r] + ak, v);
             }
             const int row = arow + (256 / KQ) * r;
             if constexpr (X6) {
@@ -717,6 +724,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                 if (n >= g.N) continue;
                 const int rb0 = wm * (BM / 2) + tm * 32 + 4 * hi;  // acc_row(r, hi) = rb0 + acc_row(r, 0)
                 float* cp = g.C + (int64_t)(m0 + rb0) * g.ldc + n;
+                if (ROWS_KO(g, 1)) continue;  // lab: no C stores
                 if (full) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) cp[acc_row(r, 0) * ldc] = acc[tm][tn][r];
@@ -1244,13 +1252,17 @@ struct RowsCfg {
 RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     const int env_bn = lab_knob("UNET_ROWS_BN", 0);
     if (env_bn > 0) return RowsCfg{env_bn, lab_knob("UNET_ROWS_BK", 16)};
+    // grids of 128 x 128 tiles that leave CUs idle (the deep levels at small batch: 2048-8192
+    // rows) take 64-wide N tiles, twice the blocks
+    const bool narrow = lab_knob("UNET_ROWS_NARROW", 1) && a.N > 64 && cdiv(a.M, 128) * cdiv(a.N, 128) < 256;
     if (amode == A_BNBWD) {
-        if (a.N <= 64) return RowsCfg{64, 32};
+        if (a.N <= 64 || narrow) return RowsCfg{64, 32};
         if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
         return RowsCfg{128, 32};
     }
     const int bk32_k = lab_knob("UNET_BK32_MIN_K", 256);  // smallest K that takes BK = 32
     if (a.N <= 64) return RowsCfg{64, 16};
+    if (narrow) return RowsCfg{64, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
     return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
@@ -1267,7 +1279,9 @@ void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
 bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
 
 template <int AMODE, bool DROP, int EPI>
-int launch_rows(const RowsArgs& a, hipStream_t st, const char* what) {
+int launch_rows(const RowsArgs& a0, hipStream_t st, const char* what) {
+    RowsArgs a = a0;
+    a.ko = lab_knob("UNET_ROWS_KO", 0);  // 1 no C stores, 2 no dz side copy, 4 no k-loop loads (lab)
     if (rows_vec_ok(a, AMODE)) {
         const RowsCfg c = rows_cfg(a, AMODE);
 #ifdef UNET_LAB_BUILD  // (not compiled into the product library)

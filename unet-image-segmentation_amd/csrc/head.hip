@@ -177,6 +177,56 @@ __global__ __launch_bounds__(256) void dice_partial_kernel(const float* __restri
     }
 }
 
+// Multi-class form: the block's pixel rows (ncls contiguous floats each) staged a 256-pixel tile
+// at a time through LDS with coalesced loads, then lane (class c, 32-row group g) sums its column
+// slice; the 8 groups are combined in a fixed order at the end.  (The one-lane-per-pixel form
+// read 21-float rows lane-strided: 77 us for the batch-8 21-class sums, profiles/r4j_cfg4_trace.txt.)
+template <int NC>
+__global__ __launch_bounds__(256) void dice_partial_m_kernel(const float* __restrict__ yt, const float* __restrict__ yp,
+                                                             int64_t hw, int ncls, int64_t ppb, float* __restrict__ part) {
+    __shared__ float Ys[256 * NC], Qs[256 * NC];
+    const int n = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+    const int c = threadIdx.x % NC, g = threadIdx.x / NC;
+    float I = 0.f, T = 0.f, P = 0.f;
+    const int64_t p0 = (int64_t)blk * ppb;
+    const int64_t p1 = p0 + ppb < hw ? p0 + ppb : hw;
+    for (int64_t t0 = p0; t0 < p1; t0 += 256) {
+        const int np = p1 - t0 < 256 ? (int)(p1 - t0) : 256;
+        const int cnt = np * ncls;
+        const int64_t f0 = ((int64_t)n * hw + t0) * ncls;
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += 256) {
+            Ys[i] = yt[f0 + i];
+            Qs[i] = yp[f0 + i];
+        }
+        __syncthreads();
+        if (g < 8 && c < ncls) {
+            const int r1 = (g + 1) * 32 < np ? (g + 1) * 32 : np;
+            for (int r = g * 32; r < r1; ++r) {
+                const float y = Ys[r * ncls + c], q = Qs[r * ncls + c];
+                I = fmaf(y, q, I);
+                T += y;
+                P += q;
+            }
+        }
+    }
+    __syncthreads();
+    if (g < 8) {
+        Ys[g * NC + c] = I;
+        Ys[8 * NC + g * NC + c] = T;
+        Ys[16 * NC + g * NC + c] = P;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * NC) {
+        const int j = threadIdx.x / NC, cc = threadIdx.x % NC;
+        if (cc < ncls) {
+            float sacc = 0.f;
+            for (int q = 0; q < 8; ++q) sacc += Ys[j * 8 * NC + q * NC + cc];
+            part[(((int64_t)n * nblk + blk) * 3 + j) * ncls + cc] = sacc;
+        }
+    }
+}
+
 // One wave per (image, class) term (the 4 waves take terms w, w + 4, ...): lane b sums the block
 // partials b, b + 64, ... in double, an xor-shuffle tree (fixed lane order) combines the lanes;
 // the dice / iou terms are then added in term order by thread 0 -- deterministic, and no thread
@@ -186,7 +236,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__global__ __launch_bounds__(256) void dice_finalize_kernel(const float* __restrict__ part, int N, int nblk, int ncls,
+__global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* __restrict__ part, int N, int nblk, int ncls,
                                                             float smooth, float* __restrict__ sums,
                                                             float* __restrict__ result) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -196,7 +246,7 @@ __global__ __launch_bounds__(256) void dice_finalize_kernel(const float* __restr
     if (threadIdx.x == 0) acc[0] = acc[1] = 0.0;
     for (int base = 0; base < N * ncls; base += kMaxTerms) {
         const int nt = N * ncls - base < kMaxTerms ? N * ncls - base : kMaxTerms;
-        for (int k = wave; k < nt; k += 4) {
+        for (int k = wave; k < nt; k += (int)(blockDim.x >> 6)) {
             const int idx = base + k, n = idx / ncls, c = idx % ncls;
             double I = 0.0, T = 0.0, P = 0.0;
             for (int b = lane; b < nblk; b += 64) {
@@ -419,6 +469,417 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(int64_t M, int64_t hw, in
     }
 }
 
+// Multi-class head forward, one pixel per thread over 256-pixel tiles (Cin <= 64): the tile's
+// activations staged through LDS with coalesced float4 loads (view applied), the kernel as
+// [Cin][NC] rows read 4 classes at a time (ds_read_b128, one address per wave: broadcast), logits
+// in NC registers (NC = the class count rounded up to 4), softmax, probabilities out.
+// (The earlier one-float-per-class LDS reads over 32 padded classes made the 21-class head
+// LDS-bound: 153 us per batch-8 forward, profiles/r4j_cfg4_trace.txt.)
+template <int MODE, int NC>
+__global__ __launch_bounds__(256) void head_fwdm_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, float* __restrict__ prob) {
+    constexpr int CMAX = 64, LA = CMAX + 4;
+    __shared__ __attribute__((aligned(16))) float Ws[CMAX * NC];
+    __shared__ __attribute__((aligned(16))) float A[256 * LA];
+    const int Cin = v.c0, CQ = Cin / 4;
+    for (int i = threadIdx.x; i < Cin * NC; i += 256) {
+        const int k = i / NC, c = i - k * NC;
+        Ws[i] = c < ncls ? W[k * ncls + c] : 0.f;
+    }
+    float bl[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) bl[c] = (c < ncls && bias) ? bias[c] : 0.f;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < 256 * CQ; idx += 256) {
+            const int p = idx / CQ, kq = idx - p * CQ;
+            const int64_t m = m0 + p;
+            const float4 x = m < M ? row_load4<MODE, false>(v, m, 4 * kq) : f4(0.f);
+            *reinterpret_cast<float4*>(&A[p * LA + 4 * kq]) = x;
+        }
+        __syncthreads();
+        const int64_t m = m0 + threadIdx.x;
+        if (m >= M) continue;
+        float l[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) l[c] = bl[c];
+        for (int k4 = 0; k4 < CQ; ++k4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(&A[threadIdx.x * LA + 4 * k4]);
+            const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float* wr = &Ws[(4 * k4 + j) * NC];
+#pragma unroll
+                for (int c4 = 0; c4 < NC / 4; ++c4) {
+                    const float4 w4 = *reinterpret_cast<const float4*>(wr + 4 * c4);
+                    l[4 * c4 + 0] = fmaf(av[j], w4.x, l[4 * c4 + 0]);
+                    l[4 * c4 + 1] = fmaf(av[j], w4.y, l[4 * c4 + 1]);
+                    l[4 * c4 + 2] = fmaf(av[j], w4.z, l[4 * c4 + 2]);
+                    l[4 * c4 + 3] = fmaf(av[j], w4.w, l[4 * c4 + 3]);
+                }
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            if (c < ncls) mx = fmaxf(mx, l[c]);
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            l[c] = c < ncls ? expf(l[c] - mx) : 0.f;
+            s += l[c];
+        }
+        const float inv = 1.0f / s;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            if (c < ncls) prob[m * ncls + c] = l[c] * inv;
+    }
+}
+
+// Multi-class head forward on the matrix cores (Cin = 8 KC <= 64, ncls <= 32): one wave per
+// 32-pixel subtile, logits^T (32 classes x 32 pixels) = W^T x^T by v_mfma_f32_32x32x2_f32 with
+// the kernel as the register-resident A operand and each lane's pixel row as B (lane (lo, hi)
+// loads channels 8t + 4hi .. + 3 of pixel lo as float4, t < KC: k step 4t + i is channel
+// 8t + 4hi + i on either operand), the bias as the accumulator's start.  Lane (lo, hi) then holds
+// 16 of pixel lo's logits (classes acc_row(r, hi)); the softmax combines the two halves with one
+// lane swap, and the wave's 32 x ncls probabilities leave through LDS as contiguous float4 runs.
+// The next subtile's rows are loaded before this one's products (software prefetch).
+// row of accumulator register r of a v_mfma_f32_32x32x2_f32 tile in lane half hi
+__device__ __forceinline__ int hx_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+template <int MODE, int KC>
+__global__ __launch_bounds__(256) void head_fwdx_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, float* __restrict__ prob,
+                                                        bool vec) {
+    __shared__ __attribute__((aligned(16))) float scs[8 * KC], shs[8 * KC];
+    __shared__ __attribute__((aligned(16))) float ob[4][32 * 32];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lo = lane & 31, hi = lane >> 5;
+    constexpr int CIN = 8 * KC;
+    if constexpr (MODE == UNET_VIEW_BNRELU) {
+        for (int i = threadIdx.x; i < CIN; i += 256) {
+            scs[i] = v.sc0[i];
+            shs[i] = v.sh0[i];
+        }
+    }
+    float wa[4 * KC];
+#pragma unroll
+    for (int t = 0; t < KC; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wa[4 * t + i] = lo < ncls ? W[(8 * t + 4 * hi + i) * ncls + lo] : 0.f;
+    float bl[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int c = hx_row(r, hi);
+        bl[r] = (c < ncls && bias) ? bias[c] : 0.f;
+    }
+    __syncthreads();
+    float* o = ob[wave];
+    const int64_t nsub = (M + 31) / 32, step = (int64_t)gridDim.x * 4;
+    int64_t sub = (int64_t)blockIdx.x * 4 + wave;
+    float4 xn[KC];
+    auto load = [&](int64_t sb) {
+        const int64_t px = sb * 32 + lo;
+#pragma unroll
+        for (int t = 0; t < KC; ++t) xn[t] = (sb < nsub && px < M) ? ld4(v.src0 + px * CIN + 8 * t + 4 * hi) : f4(0.f);
+    };
+    load(sub);
+    for (; sub < nsub; sub += step) {
+        float4 x[KC];
+#pragma unroll
+        for (int t = 0; t < KC; ++t) x[t] = xn[t];
+        load(sub + step);
+        if constexpr (MODE == UNET_VIEW_BNRELU) {
+#pragma unroll
+            for (int t = 0; t < KC; ++t)
+                x[t] = bnrelu4(x[t], *reinterpret_cast<const float4*>(&scs[8 * t + 4 * hi]),
+                               *reinterpret_cast<const float4*>(&shs[8 * t + 4 * hi]));
+        }
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = bl[r];
+#pragma unroll
+        for (int t = 0; t < KC; ++t) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * t + 0], x[t].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * t + 1], x[t].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * t + 2], x[t].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[4 * t + 3], x[t].w, acc, 0, 0, 0);
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (hx_row(r, hi) < ncls) mx = fmaxf(mx, acc[r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float e[16], sum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            e[r] = hx_row(r, hi) < ncls ? expf(acc[r] - mx) : 0.f;
+            sum += e[r];
+        }
+        sum += __shfl_xor(sum, 32, 64);
+        const float inv = 1.0f / sum;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (hx_row(r, hi) < ncls) o[lo * ncls + hx_row(r, hi)] = e[r] * inv;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t p0 = sub * 32;
+        const int cnt = (int)((M - p0 < 32 ? M - p0 : 32) * ncls);
+        float* dst = prob + p0 * ncls;
+        const int c4n = vec ? cnt >> 2 : 0;
+        for (int i = lane; i < c4n; i += 64) st4(dst + 4 * i, *reinterpret_cast<const float4*>(&o[4 * i]));
+        for (int i = 4 * c4n + lane; i < cnt; i += 64) dst[i] = o[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Multi-class head backward over 256-pixel tiles: one thread per pixel forms the softmax-backward
+// dlogit (to global for the weight gradient, and into an LDS row of NC + 4 floats), then one
+// thread per (pixel, channel quad) forms dx = W dlogit with its 4 x NC kernel values held in
+// registers and the pixel's dlogits read 4 at a time (broadcast ds_read_b128).  (The earlier form
+// re-read the kernel from LDS for every output and stored dlogit rows 32 floats apart, 32-way
+// bank conflicts: 715 us per batch-8 backward, profiles/r4j_cfg4_trace.txt.)
+template <int NC, int LOSS>
+__global__ __launch_bounds__(256) void head_bwdm_kernel(int64_t M, int64_t hw, int Cin, int ncls,
+                                                        const float* __restrict__ W, const float* __restrict__ prob,
+                                                        const float* __restrict__ yt, const float* __restrict__ sums,
+                                                        float smooth, float gscale, float* __restrict__ dlogit,
+                                                        float* __restrict__ dx) {
+    constexpr int LD = NC + 4;
+    __shared__ __attribute__((aligned(16))) float dls[256 * LD];
+    const int CQ = Cin / 4;  // divides 256 (launcher)
+    const int kq = threadIdx.x % CQ, pp = threadIdx.x / CQ, PS = 256 / CQ;
+    float wr[4][NC];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) wr[j][c] = c < ncls ? W[(4 * kq + j) * ncls + c] : 0.f;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        {
+            const int64_t m = m0 + threadIdx.x;
+            float p[NC], dl[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                p[c] = 0.f;
+                dl[c] = 0.f;
+                if (c < ncls && m < M) {
+                    p[c] = prob[m * ncls + c];
+                    dl[c] = loss_grad<LOSS>(yt[m * ncls + c], sums + ((m / hw) * ncls + c) * 3, smooth, gscale);
+                }
+            }
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) s = fmaf(dl[c], p[c], s);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                dl[c] = p[c] * (dl[c] - s);
+                if (c < ncls && m < M) dlogit[m * ncls + c] = dl[c];
+            }
+#pragma unroll
+            for (int c4 = 0; c4 < NC / 4; ++c4)
+                *reinterpret_cast<float4*>(&dls[threadIdx.x * LD + 4 * c4]) =
+                    make_float4(dl[4 * c4], dl[4 * c4 + 1], dl[4 * c4 + 2], dl[4 * c4 + 3]);
+        }
+        __syncthreads();
+        for (int p = pp; p < 256; p += PS) {
+            const int64_t m = m0 + p;
+            if (m >= M) break;
+            float4 o = f4(0.f);
+#pragma unroll
+            for (int c4 = 0; c4 < NC / 4; ++c4) {
+                const float4 d = *reinterpret_cast<const float4*>(&dls[p * LD + 4 * c4]);
+                const float dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    o.x = fmaf(wr[0][4 * c4 + i], dv[i], o.x);
+                    o.y = fmaf(wr[1][4 * c4 + i], dv[i], o.y);
+                    o.z = fmaf(wr[2][4 * c4 + i], dv[i], o.z);
+                    o.w = fmaf(wr[3][4 * c4 + i], dv[i], o.w);
+                }
+            }
+            st4(dx + m * Cin + 4 * kq, o);
+        }
+        __syncthreads();
+    }
+}
+
+// Multi-class head, fully fused backward (ncls <= 24, Cin <= 64 with Cin / 2 dividing 256) over
+// 256-pixel tiles -- one pass instead of dlogit out + a weight-gradient GEMM + a column sum (+ the
+// BN-backward statistics pass over (dx, z) of the last decoder block):
+//   stage  : the tile's prob and y_true rows (ncls contiguous floats a pixel) into LDS, float4;
+//   phase 1: one lane per pixel -> dlogit = p (dL/dp - sum_c dL/dp_c p_c), LDS rows of NC + 4;
+//   phase 2: one lane per (pixel, channel pair): dx = W dlogit with W's two rows in registers,
+//            dW += x dlogit^T in registers across tiles, (STATS) the BN-backward partials of dx;
+//            lanes < 8 NC: the tile's dlogit column sums (db), 32 rows each;
+//   end    : fixed-order LDS reductions -> per-block partials of dW (Cin x ncls), db (ncls) and
+//            (STATS) bnpart[block][0 | 1][c] = sum g | sum g xhat, g = dx [z sc + sh > 0].
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int MODE, int NC, int LOSS, bool STATS>
+__global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int64_t hw, int ncls,
+                                                         const float* __restrict__ W, const float* __restrict__ prob,
+                                                         const float* __restrict__ yt, const float* __restrict__ sums,
+                                                         float smooth, float gscale, bool vec, float* __restrict__ dx,
+                                                         float* __restrict__ part_w, float* __restrict__ part_b,
+                                                         const float* __restrict__ mu, const float* __restrict__ rs,
+                                                         float* __restrict__ bnpart) {
+    main_stream_prio();
+    constexpr int LD = NC + 4;
+    __shared__ __attribute__((aligned(16))) float Pt[256 * NC];
+    __shared__ __attribute__((aligned(16))) float Gt[256 * NC];
+    __shared__ __attribute__((aligned(16))) float dls[256 * LD];
+    const int Cin = v.c0, CP = Cin / 2;
+    const int kp = threadIdx.x % CP, pp = threadIdx.x / CP, PS = 256 / CP;
+    const int c0 = 2 * kp;
+    // the channel pair's kernel rows and weight-gradient sums as float pairs (packed FMAs)
+    f2v wr[NC], dw[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        wr[c] = c < ncls ? f2v{W[c0 * ncls + c], W[(c0 + 1) * ncls + c]} : f2v{0.f, 0.f};
+        dw[c] = f2v{0.f, 0.f};
+    }
+    float2 hsc = make_float2(1.f, 1.f), hsh = make_float2(0.f, 0.f), smu = hsh, srs = hsh, s1 = hsh, s2 = hsh;
+    if constexpr (MODE == UNET_VIEW_BNRELU) {
+        hsc = *reinterpret_cast<const float2*>(v.sc0 + c0);
+        hsh = *reinterpret_cast<const float2*>(v.sh0 + c0);
+    }
+    if constexpr (STATS) {
+        if (mu) {
+            smu = *reinterpret_cast<const float2*>(mu + c0);
+            srs = *reinterpret_cast<const float2*>(rs + c0);
+        }
+    }
+    const int dbc = threadIdx.x % NC, dbq = threadIdx.x / NC;  // db: column, 32-row group
+    float dbp = 0.f;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        const int np = M - m0 < 256 ? (int)(M - m0) : 256;
+        const int cnt = np * ncls;
+        const float* pg = prob + m0 * ncls;
+        const float* yg = yt + m0 * ncls;
+        __syncthreads();
+        const int c4n = vec ? cnt >> 2 : 0;
+        for (int i = threadIdx.x; i < c4n; i += 256) {
+            reinterpret_cast<float4*>(Pt)[i] = ld4(pg + 4 * i);
+            reinterpret_cast<float4*>(Gt)[i] = ld4(yg + 4 * i);
+        }
+        for (int i = 4 * c4n + threadIdx.x; i < cnt; i += 256) {
+            Pt[i] = pg[i];
+            Gt[i] = yg[i];
+        }
+        __syncthreads();
+        {
+            const int p = threadIdx.x;
+            float dl[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) dl[c] = 0.f;
+            if (p < np) {
+                const float* s3 = sums + ((m0 + p) / hw) * ncls * 3;
+                float s = 0.f;
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    if (c < ncls) {
+                        const float g = loss_grad<LOSS>(Gt[p * ncls + c], s3 + 3 * c, smooth, gscale);
+                        dl[c] = g;
+                        s = fmaf(g, Pt[p * ncls + c], s);
+                    }
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                    if (c < ncls) dl[c] = Pt[p * ncls + c] * (dl[c] - s);
+            }
+#pragma unroll
+            for (int c4 = 0; c4 < NC / 4; ++c4)
+                *reinterpret_cast<float4*>(&dls[p * LD + 4 * c4]) =
+                    make_float4(dl[4 * c4], dl[4 * c4 + 1], dl[4 * c4 + 2], dl[4 * c4 + 3]);
+        }
+        __syncthreads();
+        if (threadIdx.x < 8 * NC) {
+            float t = 0.f;
+            for (int q = 0; q < 32; ++q) t += dls[(dbq * 32 + q) * LD + dbc];
+            dbp += t;
+        }
+        for (int p = pp; p < np; p += PS) {
+            const int64_t m = m0 + p;
+            const float2 zr = *reinterpret_cast<const float2*>(v.src0 + m * Cin + c0);
+            float2 a = zr;
+            if constexpr (MODE == UNET_VIEW_BNRELU)
+                a = make_float2(fmaxf(fmaf(zr.x, hsc.x, hsh.x), 0.f), fmaxf(fmaf(zr.y, hsc.y, hsh.y), 0.f));
+            f2v o = {0.f, 0.f};
+            const f2v a2 = {a.x, a.y};
+#pragma unroll
+            for (int c4 = 0; c4 < NC / 4; ++c4) {
+                const float4 d = *reinterpret_cast<const float4*>(&dls[p * LD + 4 * c4]);
+                const float dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const f2v dd = {dv[i], dv[i]};
+                    o = __builtin_elementwise_fma(wr[4 * c4 + i], dd, o);
+                    dw[4 * c4 + i] = __builtin_elementwise_fma(a2, dd, dw[4 * c4 + i]);
+                }
+            }
+            const float ox = o.x, oy = o.y;
+            *reinterpret_cast<float2*>(dx + m * Cin + c0) = make_float2(ox, oy);
+            if constexpr (STATS) {
+                const float gx = a.x > 0.f ? ox : 0.f, gy = a.y > 0.f ? oy : 0.f;
+                s1.x += gx;
+                s1.y += gy;
+                s2.x = fmaf(gx, (zr.x - smu.x) * srs.x, s2.x);
+                s2.y = fmaf(gy, (zr.y - smu.y) * srs.y, s2.y);
+            }
+        }
+    }
+    // per-block partials, each a fixed-order sum over the block's lanes
+    float4* red = reinterpret_cast<float4*>(Pt);  // 256 float4 (Pt holds 256 NC >= 1024 floats)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int c4 = 0; c4 < NC / 4; ++c4) {
+            __syncthreads();
+            red[threadIdx.x] = j == 0 ? make_float4(dw[4 * c4].x, dw[4 * c4 + 1].x, dw[4 * c4 + 2].x, dw[4 * c4 + 3].x)
+                                      : make_float4(dw[4 * c4].y, dw[4 * c4 + 1].y, dw[4 * c4 + 2].y, dw[4 * c4 + 3].y);
+            __syncthreads();
+            if (threadIdx.x < CP) {
+                float4 t = red[threadIdx.x];
+                for (int q = threadIdx.x + CP; q < 256; q += CP) t = add4(t, red[q]);
+                float* o = part_w + (int64_t)blockIdx.x * Cin * ncls + (2 * threadIdx.x + j) * ncls + 4 * c4;
+                if (4 * c4 + 0 < ncls) o[0] = t.x;
+                if (4 * c4 + 1 < ncls) o[1] = t.y;
+                if (4 * c4 + 2 < ncls) o[2] = t.z;
+                if (4 * c4 + 3 < ncls) o[3] = t.w;
+            }
+        }
+    if constexpr (STATS) {
+        __syncthreads();
+        red[threadIdx.x] = make_float4(s1.x, s1.y, s2.x, s2.y);
+        __syncthreads();
+        if (threadIdx.x < CP) {
+            float4 t = red[threadIdx.x];
+            for (int q = threadIdx.x + CP; q < 256; q += CP) t = add4(t, red[q]);
+            float* o = bnpart + (int64_t)blockIdx.x * 2 * Cin + 2 * threadIdx.x;
+            o[0] = t.x;
+            o[1] = t.y;
+            o[Cin] = t.z;
+            o[Cin + 1] = t.w;
+        }
+    }
+    __syncthreads();
+    Gt[threadIdx.x] = dbp;
+    __syncthreads();
+    if (threadIdx.x < ncls) {
+        float t = 0.f;
+        for (int q = 0; q < 8; ++q) t += Gt[q * NC + threadIdx.x];
+        part_b[(int64_t)blockIdx.x * ncls + threadIdx.x] = t;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void miou_count(float tv, float q, float thr, unsigned int* h) {
+    const long long t = (long long)tv;  // Keras casts to int64 (truncation), then range-checks
+    const long long p = thr < 0.f ? (long long)q : (q > thr ? 1 : 0);
+    if (t >= 0 && t < K && p >= 0 && p < K) {
+        const int b = (int)(t * K + p);
+#pragma unroll
+        for (int i = 0; i < K * K; ++i) h[i] += b == i ? 1u : 0u;
+    }
+}
+// K x K confusion counts, float4 loads (four elements a lane per load pair; the count % 4 tail by
+// the first threads)
 template <int K>
 __global__ __launch_bounds__(256) void meaniou_small_kernel(const float* __restrict__ yt, const float* __restrict__ yp,
                                                             int64_t count, float thr,
@@ -426,14 +887,17 @@ __global__ __launch_bounds__(256) void meaniou_small_kernel(const float* __restr
     unsigned int h[K * K];
 #pragma unroll
     for (int i = 0; i < K * K; ++i) h[i] = 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256) {
-        const long long t = (long long)yt[i];
-        const float q = yp[i];
-        const long long p = thr < 0.f ? (long long)q : (q > thr ? 1 : 0);
-        if (t >= 0 && t < K && p >= 0 && p < K) {
-#pragma unroll
-            for (int b = 0; b < K * K; ++b) h[b] += (t * K + p == b) ? 1u : 0u;
-        }
+    const int64_t n4 = count / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 t = ld4(yt + 4 * i), q = ld4(yp + 4 * i);
+        miou_count<K>(t.x, q.x, thr, h);
+        miou_count<K>(t.y, q.y, thr, h);
+        miou_count<K>(t.z, q.z, thr, h);
+        miou_count<K>(t.w, q.w, thr, h);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < count - 4 * n4) {
+        const int64_t i = 4 * n4 + threadIdx.x;
+        miou_count<K>(yt[i], yp[i], thr, h);
     }
     __shared__ unsigned int red[4][K * K];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -529,6 +993,40 @@ extern "C" int unet_head_fwd(const unet_view* x, int n, int h, int w, int ncls, 
         UNET_CHECK_LAUNCH("unet_head_fwd");
         return 0;
     }
+    if (ncls > 1 && (x->c0 == 16 || x->c0 == 32 || x->c0 == 64) && ((uintptr_t)x->src0 % 16) == 0) {
+        // multi-class on the matrix cores
+        const int grid = (int)(cdiv(M, (int64_t)128) > 2048 ? 2048 : cdiv(M, (int64_t)128));
+        const bool vec = (uintptr_t)prob % 16 == 0;
+#define UNET_HFX(MODE_)                                                                                       \
+    switch (x->c0) {                                                                                        \
+        case 16: head_fwdx_kernel<MODE_, 2><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob, vec); break; \
+        case 32: head_fwdx_kernel<MODE_, 4><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob, vec); break; \
+        default: head_fwdx_kernel<MODE_, 8><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob, vec); break; \
+    }
+        if (x->mode == UNET_VIEW_BNRELU) UNET_HFX(UNET_VIEW_BNRELU)
+        else UNET_HFX(UNET_VIEW_PLAIN)
+#undef UNET_HFX
+        UNET_CHECK_LAUNCH("unet_head_fwd");
+        return 0;
+    }
+    if (ncls > 1 && x->c0 <= 64 && x->c0 % 4 == 0) {  // multi-class: the register-logit kernel
+        const int grid = grid_for(M, 4096);
+#define UNET_HFM(MODE_, NC_) head_fwdm_kernel<MODE_, NC_><<<grid, 256, 0, st>>>(v, M, ncls, kernel, bias, prob)
+#define UNET_HFM_NC(MODE_)                                                                \
+    do {                                                                                  \
+        if (ncls <= 4) UNET_HFM(MODE_, 4);                                                \
+        else if (ncls <= 8) UNET_HFM(MODE_, 8);                                           \
+        else if (ncls <= 16) UNET_HFM(MODE_, 16);                                         \
+        else if (ncls <= 24) UNET_HFM(MODE_, 24);                                         \
+        else UNET_HFM(MODE_, 32);                                                         \
+    } while (0)
+        if (x->mode == UNET_VIEW_BNRELU) UNET_HFM_NC(UNET_VIEW_BNRELU);
+        else UNET_HFM_NC(UNET_VIEW_PLAIN);
+#undef UNET_HFM_NC
+#undef UNET_HFM
+        UNET_CHECK_LAUNCH("unet_head_fwd");
+        return 0;
+    }
     const int TP = (ncls > 1 ? 4096 : 8192) / x->c0 < 256 ? (ncls > 1 ? 4096 : 8192) / x->c0 : 256;
     int64_t g = cdiv(M, TP);
     const int grid = (int)(g > 4096 ? 4096 : g);
@@ -568,10 +1066,18 @@ extern "C" int unet_dice_fwd(const float* y_true, const float* y_pred, int n, in
     dim3 grid(d.nblk, n);
     if (ncls == 1)
         dice_partial_kernel<1><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    else if (ncls <= 4)
+        dice_partial_m_kernel<4><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    else if (ncls <= 8)
+        dice_partial_m_kernel<8><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    else if (ncls <= 16)
+        dice_partial_m_kernel<16><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+    else if (ncls <= 24)
+        dice_partial_m_kernel<24><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
     else
-        dice_partial_kernel<kMaxCls><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
+        dice_partial_m_kernel<32><<<grid, 256, 0, st>>>(y_true, y_pred, hw, ncls, d.ppb, part);
     UNET_CHECK_LAUNCH("unet_dice_fwd(partial)");
-    dice_finalize_kernel<<<1, 256, 0, st>>>(part, n, d.nblk, ncls, smooth, sums, result);
+    dice_finalize_kernel<<<1, n * ncls >= 64 ? 1024 : 256, 0, st>>>(part, n, d.nblk, ncls, smooth, sums, result);
     UNET_CHECK_LAUNCH("unet_dice_fwd(finalize)");
     return 0;
 }
@@ -582,7 +1088,7 @@ extern "C" size_t unet_head_bwd_workspace(int n, int h, int w, int cin, int ncls
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
     size_t a = head_wgrad_workspace(M, cin, ncls);
     size_t b = colsum_workspace(M, ncls);
-    const size_t fused = align_up((size_t)1024 * cin, 64) * sizeof(float) + 1024 * sizeof(float);
+    const size_t fused = (align_up((size_t)1024 * cin * ncls, 64) + align_up((size_t)1024 * ncls, 64)) * sizeof(float);
     const size_t gen = dl + (a > b ? a : b);
     return align_up(fused > gen ? fused : gen, 256);
 }
@@ -592,6 +1098,14 @@ int head_bwd_grid(int64_t M) {
     const int64_t g = cdiv(M, 256);
     return (int)(g > 1024 ? 1024 : g);
 }
+// the fused multi-class backward (head_bwdmf_kernel) covers this head
+bool head_bwdmf_ok(const unet_view* x, int ncls) {
+    return ncls > 1 && ncls <= 24 && x->c0 <= 64 && x->c0 % 4 == 0 && 256 % (x->c0 / 2) == 0;
+}
+int head_bwdmf_grid(int64_t M) {  // 2 blocks a CU (77 KB of LDS at 24 classes): one wave of blocks
+    const int64_t g = cdiv(M, 256);
+    return (int)(g > 512 ? 512 : g);
+}
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
                   const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
                   float* dkernel, float* dbias, void* ws, size_t ws_bytes, const float* mu, const float* rs,
@@ -599,8 +1113,9 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
 }  // namespace
 
 extern "C" int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls) {
-    if (!x || x->mode != UNET_VIEW_BNRELU || ncls != 1 || n <= 0 || h <= 0 || w <= 0) return 0;
-    if (x->c0 % 4 || x->c0 > kMaxCin || 256 % (x->c0 / 4)) return 0;
+    if (!x || x->mode != UNET_VIEW_BNRELU || n <= 0 || h <= 0 || w <= 0) return 0;
+    if (ncls > 1) return head_bwdmf_ok(x, ncls) ? head_bwdmf_grid((int64_t)n * h * w) : 0;
+    if (ncls != 1 || x->c0 % 4 || x->c0 > kMaxCin || 256 % (x->c0 / 4)) return 0;
     return head_bwd_grid((int64_t)n * h * w);
 }
 
@@ -611,7 +1126,9 @@ extern "C" int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, in
                                      const float* rstd, float* bn_partials, void* ws, size_t ws_bytes,
                                      unet_stream_t stream) {
     UNET_CHECK_ARG(unet_head_bwd_bnstats_slabs(x, n, h, w, ncls) > 0,
-                   "unet_head_bwd_bnstats: needs a binary head on a BNRELU view with Cin %% 4 == 0");
+                   "unet_head_bwd_bnstats: needs a BNRELU view with Cin %% 4 == 0 (multi-class: <= 24 classes, "
+                   "Cin <= 64)");
+    UNET_CHECK_ARG(ncls == 1 || dlogit == nullptr, "unet_head_bwd_bnstats: the dlogit form is binary-only");
     UNET_CHECK_ARG(bn_partials, "unet_head_bwd_bnstats: null bn_partials");
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_head_bwd_bnstats: mean and rstd go together");
     UNET_CHECK_ARG((dx == nullptr) != (dlogit == nullptr), "unet_head_bwd_bnstats: give exactly one of dx, dlogit");
@@ -686,6 +1203,38 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
         if (rc) return rc;
         return reduce_slabs(part_b, grid, 1, dbias, 1, 1, st);
     }
+    if (head_bwdmf_ok(x, ncls)) {
+        const int grid = head_bwdmf_grid(M);
+        float* part_w = static_cast<float*>(ws);
+        float* part_b = part_w + align_up((size_t)grid * x->c0 * ncls, 64);
+        const bool vec = ((uintptr_t)prob | (uintptr_t)y_true) % 16 == 0;
+#define UNET_HMF(MODE_, NC_, L_, S_)                                                                            \
+    head_bwdmf_kernel<MODE_, NC_, L_, S_><<<grid, 256, 0, st>>>(v, M, hw, ncls, kernel, prob, y_true, sums, smooth, \
+                                                              gscale, vec, dx, part_w, part_b, mu, rs, bnpart)
+#define UNET_HMF_NC(MODE_, L_, S_)                   \
+    do {                                             \
+        if (ncls <= 4) UNET_HMF(MODE_, 4, L_, S_);   \
+        else if (ncls <= 8) UNET_HMF(MODE_, 8, L_, S_);  \
+        else if (ncls <= 16) UNET_HMF(MODE_, 16, L_, S_); \
+        else UNET_HMF(MODE_, 24, L_, S_);            \
+    } while (0)
+#define UNET_HMF_L(MODE_, S_)                                            \
+    do {                                                                 \
+        if (loss_kind == UNET_LOSS_DICE) UNET_HMF_NC(MODE_, UNET_LOSS_DICE, S_); \
+        else UNET_HMF_NC(MODE_, UNET_LOSS_IOU, S_);                     \
+    } while (0)
+        if (bnpart) UNET_HMF_L(UNET_VIEW_BNRELU, true);
+        else if (x->mode == UNET_VIEW_BNRELU) UNET_HMF_L(UNET_VIEW_BNRELU, false);
+        else UNET_HMF_L(UNET_VIEW_PLAIN, false);
+#undef UNET_HMF_L
+#undef UNET_HMF_NC
+#undef UNET_HMF
+        UNET_CHECK_LAUNCH("unet_head_bwd");
+        const int64_t L = (int64_t)x->c0 * ncls;
+        int rc = reduce_slabs(part_w, grid, L, dkernel, L, L, st);
+        if (rc) return rc;
+        return reduce_slabs(part_b, grid, ncls, dbias, ncls, ncls, st);
+    }
     float* dlg = static_cast<float*>(ws);
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);
     void* ws2 = static_cast<char*>(ws) + dl;
@@ -695,7 +1244,24 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
 #define UNET_HB(NC, L)                                                                                        \
     head_bwd_kernel<NC, L><<<grid, 256, 0, st>>>(M, hw, x->c0, ncls, kernel, prob, y_true, sums, smooth, gscale, \
                                                  dlg, dx)
-    if (ncls == 1) {
+    if (ncls > 1 && 256 % CQ == 0) {  // multi-class: kernel in registers, dlogit rows in LDS
+        const int gridm = (int)(cdiv(M, 256) > 2048 ? 2048 : cdiv(M, 256));
+#define UNET_HBM(NC_, L_)                                                                                     \
+    head_bwdm_kernel<NC_, L_><<<gridm, 256, 0, st>>>(M, hw, x->c0, ncls, kernel, prob, y_true, sums, smooth, \
+                                                     gscale, dlg, dx)
+#define UNET_HBM_NC(L_)                                        \
+    do {                                                       \
+        if (ncls <= 4) UNET_HBM(4, L_);                        \
+        else if (ncls <= 8) UNET_HBM(8, L_);                   \
+        else if (ncls <= 16) UNET_HBM(16, L_);                 \
+        else if (ncls <= 24) UNET_HBM(24, L_);                 \
+        else UNET_HBM(32, L_);                                 \
+    } while (0)
+        if (loss_kind == UNET_LOSS_DICE) UNET_HBM_NC(UNET_LOSS_DICE);
+        else UNET_HBM_NC(UNET_LOSS_IOU);
+#undef UNET_HBM_NC
+#undef UNET_HBM
+    } else if (ncls == 1) {
         if (loss_kind == UNET_LOSS_DICE) UNET_HB(1, UNET_LOSS_DICE);
         else UNET_HB(1, UNET_LOSS_IOU);
     } else {
@@ -719,8 +1285,8 @@ extern "C" int unet_meaniou_update(const float* y_true, const float* y_pred, int
     hipStream_t st = as_stream(stream);
     const int grid = grid_for(count, 2048);
     auto* conf = reinterpret_cast<unsigned long long*>(confusion);
-    if (num_classes == 2)
-        meaniou_small_kernel<2><<<grid, 256, 0, st>>>(y_true, y_pred, count, threshold, conf);
+    if (num_classes == 2 && ((uintptr_t)y_true | (uintptr_t)y_pred) % 16 == 0)
+        meaniou_small_kernel<2><<<grid_for(cdiv(count, 4), 2048), 256, 0, st>>>(y_true, y_pred, count, threshold, conf);
     else
         meaniou_kernel<<<grid, 256, 0, st>>>(y_true, y_pred, count, num_classes, threshold, conf);
     UNET_CHECK_LAUNCH("unet_meaniou_update");

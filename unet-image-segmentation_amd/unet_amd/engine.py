@@ -645,7 +645,7 @@ class UNetEngine:
         if S > 0:  # the head's dx is all of the last block's da: emit its BN-backward partials too
             # binary head feeding the fused block backward: da = dlogit (x) kernel stays rank one
             # (one float per pixel stored instead of the 64-channel da, formed again on load)
-            rank1 = self._fused_bwd(last, lb)
+            rank1 = self.num_classes == 1 and self._fused_bwd(last, lb)
             if rank1 and (lb.dlogit is None or lb.dlogit.numel() != n * self.h * self.w):
                 lb.dlogit = torch.empty(n * self.h * self.w, dtype=torch.float32, device=self.device)
             ops.head_bwd_bnstats(hv, n, self.h, self.w, self.num_classes, self.vars["output_mask/kernel"], A.prob,
