@@ -236,13 +236,23 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* __restrict__ part, int N, int nblk, int ncls,
+__global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* part, int N, int nblk, int ncls,
                                                             float smooth, float* __restrict__ sums,
                                                             float* __restrict__ result) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     constexpr int kMaxTerms = 1024;  // terms kept in LDS for the ordered sum (N * ncls beyond: second pass)
     __shared__ float td[kMaxTerms], ti[kMaxTerms];
     __shared__ double acc[2];
+    // all partials staged in LDS with coalesced loads when they fit: the per-term walks
+    // then wait on LDS, not on a dependent global load a term
+    constexpr int kStage = 34816;  // 136 KB
+    __shared__ float pst[kStage];
+    const int64_t total = (int64_t)N * nblk * 3 * ncls;
+    if (total <= kStage) {
+        for (int i = threadIdx.x; i < (int)total; i += blockDim.x) pst[i] = part[i];
+        __syncthreads();
+        part = pst;
+    }
     if (threadIdx.x == 0) acc[0] = acc[1] = 0.0;
     for (int base = 0; base < N * ncls; base += kMaxTerms) {
         const int nt = N * ncls - base < kMaxTerms ? N * ncls - base : kMaxTerms;
@@ -719,7 +729,7 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
                                                          float smooth, float gscale, bool vec, float* __restrict__ dx,
                                                          float* __restrict__ part_w, float* __restrict__ part_b,
                                                          const float* __restrict__ mu, const float* __restrict__ rs,
-                                                         float* __restrict__ bnpart) {
+                                                         float* __restrict__ bnpart, int ko) {
     main_stream_prio();
     constexpr int LD = NC + 4;
     __shared__ __attribute__((aligned(16))) float Pt[256 * NC];
@@ -755,9 +765,22 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
         const float* yg = yt + m0 * ncls;
         __syncthreads();
         const int c4n = vec ? cnt >> 2 : 0;
-        for (int i = threadIdx.x; i < c4n; i += 256) {
-            reinterpret_cast<float4*>(Pt)[i] = ld4(pg + 4 * i);
-            reinterpret_cast<float4*>(Gt)[i] = ld4(yg + 4 * i);
+        for (int i0 = threadIdx.x; i0 < c4n; i0 += 256 * 3) {  // 3 + 3 float4 loads in flight
+            float4 tp[3], ty[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int i = i0 + 256 * u;
+                tp[u] = i < c4n && !(ko & 8) ? ld4(pg + 4 * i) : f4(0.5f);
+                ty[u] = i < c4n && !(ko & 8) ? ld4(yg + 4 * i) : f4(0.5f);
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int i = i0 + 256 * u;
+                if (i < c4n) {
+                    reinterpret_cast<float4*>(Pt)[i] = tp[u];
+                    reinterpret_cast<float4*>(Gt)[i] = ty[u];
+                }
+            }
         }
         for (int i = 4 * c4n + threadIdx.x; i < cnt; i += 256) {
             Pt[i] = pg[i];
@@ -769,13 +792,13 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
             float dl[NC];
 #pragma unroll
             for (int c = 0; c < NC; ++c) dl[c] = 0.f;
-            if (p < np) {
+            if (p < np && !(ko & 64)) {
                 const float* s3 = sums + ((m0 + p) / hw) * ncls * 3;
                 float s = 0.f;
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
                     if (c < ncls) {
-                        const float g = loss_grad<LOSS>(Gt[p * ncls + c], s3 + 3 * c, smooth, gscale);
+                        const float g = (ko & 1) ? Gt[p * ncls + c] : loss_grad<LOSS>(Gt[p * ncls + c], s3 + 3 * c, smooth, gscale);
                         dl[c] = g;
                         s = fmaf(g, Pt[p * ncls + c], s);
                     }
@@ -789,21 +812,41 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
                     make_float4(dl[4 * c4], dl[4 * c4 + 1], dl[4 * c4 + 2], dl[4 * c4 + 3]);
         }
         __syncthreads();
-        if (threadIdx.x < 8 * NC) {
+        if (threadIdx.x < 8 * NC && !(ko & 16)) {
             float t = 0.f;
             for (int q = 0; q < 32; ++q) t += dls[(dbq * 32 + q) * LD + dbc];
             dbp += t;
         }
-        for (int p = pp; p < np; p += PS) {
+        // input pairs four pixels at a time, the next four loaded before this four's dx stores
+        // (vmcnt counts stores too: a load issued after a store waits for it)
+        constexpr int U = 4;
+        float2 zq[U];
+        auto zload = [&](int pb) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                zq[u] = pb + u * PS < np && !(ko & 2)
+                            ? *reinterpret_cast<const float2*>(v.src0 + (m0 + pb + u * PS) * Cin + c0)
+                            : make_float2(0.5f, 0.5f);
+        };
+        zload(pp);
+        for (int pb = pp; pb < np; pb += U * PS) {
+            float2 zc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) zc[u] = zq[u];
+            if (pb + U * PS < np) zload(pb + U * PS);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+            const int p = pb + u * PS;
+            if (p >= np) break;
             const int64_t m = m0 + p;
-            const float2 zr = *reinterpret_cast<const float2*>(v.src0 + m * Cin + c0);
+            const float2 zr = zc[u];
             float2 a = zr;
             if constexpr (MODE == UNET_VIEW_BNRELU)
                 a = make_float2(fmaxf(fmaf(zr.x, hsc.x, hsh.x), 0.f), fmaxf(fmaf(zr.y, hsc.y, hsh.y), 0.f));
             f2v o = {0.f, 0.f};
             const f2v a2 = {a.x, a.y};
 #pragma unroll
-            for (int c4 = 0; c4 < NC / 4; ++c4) {
+            for (int c4 = 0; c4 < ((ko & 32) ? 0 : NC / 4); ++c4) {
                 const float4 d = *reinterpret_cast<const float4*>(&dls[p * LD + 4 * c4]);
                 const float dv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
@@ -814,13 +857,14 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
                 }
             }
             const float ox = o.x, oy = o.y;
-            *reinterpret_cast<float2*>(dx + m * Cin + c0) = make_float2(ox, oy);
+            if (!(ko & 4)) *reinterpret_cast<float2*>(dx + m * Cin + c0) = make_float2(ox, oy);
             if constexpr (STATS) {
                 const float gx = a.x > 0.f ? ox : 0.f, gy = a.y > 0.f ? oy : 0.f;
                 s1.x += gx;
                 s1.y += gy;
                 s2.x = fmaf(gx, (zr.x - smu.x) * srs.x, s2.x);
                 s2.y = fmaf(gy, (zr.y - smu.y) * srs.y, s2.y);
+            }
             }
         }
     }
@@ -1208,9 +1252,10 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
         float* part_w = static_cast<float*>(ws);
         float* part_b = part_w + align_up((size_t)grid * x->c0 * ncls, 64);
         const bool vec = ((uintptr_t)prob | (uintptr_t)y_true) % 16 == 0;
+        const int ko = lab_knob("UNET_HEAD_KO", 0);  // lab timing knock-outs (0 in the product)
 #define UNET_HMF(MODE_, NC_, L_, S_)                                                                            \
     head_bwdmf_kernel<MODE_, NC_, L_, S_><<<grid, 256, 0, st>>>(v, M, hw, ncls, kernel, prob, y_true, sums, smooth, \
-                                                              gscale, vec, dx, part_w, part_b, mu, rs, bnpart)
+                                                              gscale, vec, dx, part_w, part_b, mu, rs, bnpart, ko)
 #define UNET_HMF_NC(MODE_, L_, S_)                   \
     do {                                             \
         if (ncls <= 4) UNET_HMF(MODE_, 4, L_, S_);   \
