@@ -35,7 +35,7 @@ OPS = {
     "unet_pointwise_fwd": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 1(, (true|false))?>|gemm_rows_kernel<\d+, \d+, 0, false, 1>",
     "unet_pointwise_bwd_data": r"gemm_rows_vec<\d+, \d+, \d+, 0, false, 0(, (true|false))?>|gemm_rows_kernel<\d+, \d+, 0, false, 0>",
     "unet_pointwise_bwd_filter": r"gemm_wgrad_(vec|kernel)<\d+, \d+, 0, false, 0, false(, (true|false))?>",
-    "unet_sepconv_fwd": r"sepconv_(fwd|rk)_kernel<",
+    "unet_sepconv_fwd": r"sepconv_(fwd|rk|px)_kernel<",
     "unet_sepconv_bwd_filter": r"sepconv_wgrad_kernel<",
     "unet_pointwise_bwd_data_bnrelu": r"gemm_rows_vec<\d+, \d+, \d+, 3, (true|false), 0, (true|false)(, (true|false))?>",
     "unet_conv_transpose2x2_bwd_data_bnstats": r"gemm_rows_vec<\d+, \d+, \d+, 2, false, 3, (true|false)(, (true|false))?>",

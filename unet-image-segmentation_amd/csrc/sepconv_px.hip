@@ -98,6 +98,18 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
         }
     }
 
+    // zsel: the sign bits of gamma at this lane's epilogue columns (tn * 32 + 4 (lane & 7) + i ->
+    // bit 4 tn + i), read once here -- a gamma load inside the tile loop's epilogue made the wave
+    // wait for every load and store it had in flight (vmcnt(0)), the prefetched stages included
+    unsigned gneg = 0;
+    if (g.zsel && g.gamma) {
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const float4 gm = ld4(g.gamma + tn * 32 + 4 * (lane & 7));
+            gneg |= ((signbit(gm.x) ? 1u : 0u) | (signbit(gm.y) ? 2u : 0u) | (signbit(gm.z) ? 4u : 0u) |
+                     (signbit(gm.w) ? 8u : 0u)) << (4 * tn);
+        }
+    }
     __syncthreads();  // taps / affine visible before the first stage's staging reads them
 
     // ---- staging: set p holds stage s's halo (HR float4 / thread) and B chunks (BXC / thread)
@@ -296,12 +308,12 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
                 const float4 c = *reinterpret_cast<const float4*>(T + (16 + ((c0 + 2) & 15)) * PTLD + 4 * qd);
                 const float4 d = *reinterpret_cast<const float4*>(T + (16 + ((c1 + 2) & 15)) * PTLD + 4 * qd);
                 const int col = cb + 4 * qd;
-                const float4 gm = g.gamma ? ld4(g.gamma + col) : f4(0.f);
+                const unsigned gb = gneg >> (4 * tn);
                 float4 o;
-                o.x = pool_sel(a.x, b.x, c.x, d.x, signbit(gm.x));
-                o.y = pool_sel(a.y, b.y, c.y, d.y, signbit(gm.y));
-                o.z = pool_sel(a.z, b.z, c.z, d.z, signbit(gm.z));
-                o.w = pool_sel(a.w, b.w, c.w, d.w, signbit(gm.w));
+                o.x = pool_sel(a.x, b.x, c.x, d.x, (gb & 1u) != 0);
+                o.y = pool_sel(a.y, b.y, c.y, d.y, (gb & 2u) != 0);
+                o.z = pool_sel(a.z, b.z, c.z, d.z, (gb & 4u) != 0);
+                o.w = pool_sel(a.w, b.w, c.w, d.w, (gb & 8u) != 0);
                 const int H2 = g.H >> 1, W2 = g.W >> 1;
                 st4(g.zsel + ((int64_t)(n * H2 + (h0 >> 1) + wave) * W2 + (w0 >> 1) + j) * g.Cout + col, o);
             }
