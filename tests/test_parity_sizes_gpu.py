@@ -208,7 +208,7 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
       * loss and dice within 1e-5;
       * every block's BatchNorm batch mean / variance (1,048,576 pixels per channel at 256 x 16)
         within 1e-4 relative to the channel's scale;
-      * every gradient tensor on its strided subsample within relative L2 max(2e-3, 2 e32), e32 =
+      * every gradient tensor on its strided subsample within relative L2 max(2e-3, e32), e32 =
         the float32 oracle's own distance to float64 there; norms within 1e-2;
       * post-AdamW values as test_train_step_128_batch4 (first 128 per variable) and the moving
         statistics."""
@@ -249,7 +249,7 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
         got = flat[MG.sub_index(flat.size)]
         e = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
         errs[k] = e
-        lim = max(2e-3, 2.0 * float(g["e32sub:" + k]))
+        lim = max(2e-3, float(g["e32sub:" + k]))  # (2 e32 through round 3; worst ratio seen 0.53)
         if e > lim:
             bad[k] = (e, lim)
     worst = sorted(errs.items(), key=lambda r: -r[1])[:5]
@@ -290,3 +290,43 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
             assert np.abs(got - own)[~sure].max(initial=0.0) <= tol, name
     del m
     torch.cuda.empty_cache()
+
+
+def test_split_precision_relu_decisions_train256c21():
+    """Why the split-precision forward moves train256c21's worst gradient (bneck_block1 pointwise:
+    7.5e-3 with the fp32-MFMA forward, 1.46e-2 with bf16x6): the two forwards
+    of the same step differ by float rounding only (bf16x6 products are exact, their sum order is
+    not fmaf's), and a ReLU pre-activation within that rounding of 0 takes the other decision,
+    routing its gradient differently.  Counts, per block, the pixels x channels whose ReLU decision
+    differs between the two device forwards, and the two forwards' gradient distance per tensor
+    (both logged); asserts the flips stay a rounding-level fraction of the decisions."""
+    from unet_amd.model import UNetModel
+    from unet_amd.optim import AdamW
+    g = _load("train256c21.npz")
+    size, n, ncls = int(g["size"]), int(g["n"]), int(g["ncls"])
+    w = MG.model_weights(ncls, MG.FULL, int(g["w_seed"]))
+    x = MG.U(int(g["x_seed"]), (n, size, size, 3)).astype(np.float32)
+    y = MG.class_masks(n, size, size, ncls, int(g["x_seed"]) + 1).astype(np.float32)
+    runs = []
+    for x3 in (False, True):
+        m = UNetModel((size, size, 3), ncls, dropout_rate=0.0)
+        m.engine.use_x3 = x3
+        m.engine.set_weights_dict({k: v.astype(np.float32) for k, v in w.items()})
+        m.compile(AdamW(2e-3, 1e-4), "dice_loss")
+        m.train_step(x, y)
+        torch.cuda.synchronize()
+        A = m.engine._acts_last
+        dec = {b.name: ((A.blocks[b.name].z * A.blocks[b.name].scale + A.blocks[b.name].shift) > 0)
+               for b in m.engine.blocks}
+        grads = {k: host(t).astype(np.float64) for k, t in m.engine.gvars.items()}
+        runs.append((dec, grads))
+        del m, A
+        torch.cuda.empty_cache()
+    flips = {b: int((runs[0][0][b] != runs[1][0][b]).sum()) for b in runs[0][0]}
+    total = sum(int(v.numel()) for v in runs[0][0].values())
+    gd = {k: float(np.linalg.norm(runs[1][1][k] - runs[0][1][k]) / max(np.linalg.norm(runs[0][1][k]), 1e-30))
+          for k in runs[0][1]}
+    worst = sorted(gd.items(), key=lambda r: -r[1])[:5]
+    _log({"test": "x3_vs_fp32_relu_decisions[train256c21]", "relu_flips_per_block": flips,
+          "flips_total": sum(flips.values()), "elements": total, "grad_rel_l2_x3_vs_fp32_worst": worst})
+    assert sum(flips.values()) <= 1e-5 * total, flips

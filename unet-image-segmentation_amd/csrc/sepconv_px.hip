@@ -382,9 +382,7 @@ void launch_px_t(const SepArgs& a, bool stats, bool write_y, int ntiles, int gri
 template <int MODE, bool DROP, int PD>
 void launch_px_p(const SepArgs& a, bool stats, bool write_y, int ntiles, int grid, hipStream_t st) {
     if (a.Cout == 64) {
-#ifdef UNET_LAB_BUILD  // 64 -> 64: lab only (px_supported)
         if (a.Cin == 64) { launch_px_t<MODE, DROP, 64, 64, PD>(a, stats, write_y, ntiles, grid, st); return; }
-#endif
         launch_px_t<MODE, DROP, 64, 128, PD>(a, stats, write_y, ntiles, grid, st);
     } else {
         if (a.Cin == 64) launch_px_t<MODE, DROP, 128, 64, PD>(a, stats, write_y, ntiles, grid, st);
@@ -407,9 +405,10 @@ bool px_supported(const SepArgs& a, int mode) {
     if (!a.pkx) return false;
     if (mode != UNET_VIEW_PLAIN && mode != UNET_VIEW_BNRELU && mode != UNET_VIEW_CONCAT) return false;
     if ((a.Cin != 64 && a.Cin != 128) || (a.Cout != 64 && a.Cout != 128)) return false;
-    // 64 -> 64 stays on the one-tile kernel: it runs 3 blocks per CU there (42 KB of LDS, <= 168
-    // VGPRs) against 2 here, and measured 4-5 % faster on enc1_block2 (profiles/r4b_px_lab.log)
-    if (a.Cin == 64 && a.Cout == 64 && lab_knob("UNET_PX_6464", 0) == 0) return false;
+    // 64 -> 64 too since the epilogue stopped draining the prefetch (gamma signs read once):
+    // enc1_block2 1.09x, dec1_block2 1.14x the one-tile kernel (profiles/r4l_px_lab.log; it was
+    // 0.96x before, r4b).  UNET_PX_6464=0 (lab) keeps 64 -> 64 on the one-tile kernel.
+    if (a.Cin == 64 && a.Cout == 64 && lab_knob("UNET_PX_6464", 1) == 0) return false;
     if (mode == UNET_VIEW_CONCAT && a.x.c0 % 16) return false;
     return a.H % TH == 0 && a.W % TW == 0;
 }
