@@ -388,12 +388,13 @@ int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
                   int loss_kind, float loss_scale, float* dx, float* dkernel,
                   float* dbias,
                   void* ws, size_t ws_bytes, unet_stream_t stream);
-/* Binary head on a BNRELU view: unet_head_bwd plus the BatchNorm-backward
+/* Head on a BNRELU view (binary; or multi-class with <= 24 classes and
+ * Cin <= 64, one fused pass): unet_head_bwd plus the BatchNorm-backward
  * partial sums of the head input's block (dx is all of its da; bn_partials
  * layout and finish as unet_dwconv3x3_bwd_data_bnstats).  _slabs: S, or 0.
- * dx may be NULL when dlogit (m floats) is given: dx = dlogit (x) kernel is
- * rank one, so only dL/dlogit per pixel is stored and the consumer forms dx
- * on load (unet_sepconv_bwd_fused's da_dlogit; ABI 10).                     */
+ * Binary only: dx may be NULL when dlogit (m floats) is given: dx = dlogit
+ * (x) kernel is rank one, so only dL/dlogit per pixel is stored and the
+ * consumer forms dx on load (unet_sepconv_bwd_fused's da_dlogit; ABI 10).   */
 int unet_head_bwd_bnstats_slabs(const unet_view* x, int n, int h, int w, int ncls);
 int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, int ncls,
                           const float* kernel, const float* prob,
