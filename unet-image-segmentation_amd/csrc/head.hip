@@ -249,7 +249,17 @@ __global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* part, 
     __shared__ float pst[kStage];
     const int64_t total = (int64_t)N * nblk * 3 * ncls;
     if (total <= kStage) {
-        for (int i = threadIdx.x; i < (int)total; i += blockDim.x) pst[i] = part[i];
+        // 8 independent loads in flight per thread (a load-store pair per iteration exposed the
+        // load latency ~32 times: 31 us for 8 x 21-class partials)
+        const int bd = blockDim.x;
+        for (int i0 = threadIdx.x; i0 < (int)total; i0 += 8 * bd) {
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = i0 + u * bd < (int)total ? part[i0 + u * bd] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i0 + u * bd < (int)total) pst[i0 + u * bd] = t[u];
+        }
         __syncthreads();
         part = pst;
     }
