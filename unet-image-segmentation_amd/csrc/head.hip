@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void head_fwdm_kernel(DView v, int64_t M, int 
 // row of accumulator register r of a v_mfma_f32_32x32x2_f32 tile in lane half hi
 __device__ __forceinline__ int hx_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 template <int MODE, int KC>
-__global__ __launch_bounds__(256, 3) void head_fwdx_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
+__global__ __launch_bounds__(256) void head_fwdx_kernel(DView v, int64_t M, int ncls, const float* __restrict__ W,
                                                         const float* __restrict__ bias, float* __restrict__ prob,
                                                         bool vec) {
     __shared__ __attribute__((aligned(16))) float scs[8 * KC], shs[8 * KC];
@@ -721,25 +721,19 @@ __global__ __launch_bounds__(256) void head_bwdm_kernel(int64_t M, int64_t hw, i
     }
 }
 
-// Multi-class head, fully fused backward (ncls <= 24, Cin <= 64) over 128-pixel tiles -- one pass
-// instead of dlogit out + a weight-gradient GEMM + a column sum (+ the BN-backward statistics pass
-// over (dx, z) of the last decoder block):
+// Multi-class head, fully fused backward (ncls <= 24, Cin <= 64 with Cin / 2 dividing 256) over
+// 256-pixel tiles -- one pass instead of dlogit out + a weight-gradient GEMM + a column sum (+ the
+// BN-backward statistics pass over (dx, z) of the last decoder block):
 //   stage  : the tile's prob and y_true rows (ncls contiguous floats a pixel) into LDS, float4;
 //   phase 1: one lane per pixel -> dlogit = p (dL/dp - sum_c dL/dp_c p_c), LDS rows of NC + 4;
-//   phase 2: one lane per (pixel, channel pair, class half): the pair's kernel rows for its NC / H
-//            classes in registers, the partial dx = W dlogit over those classes (the two halves
-//            combined with one lane swap, a + b == b + a: both lanes hold the same sum), each lane
-//            storing one channel; dW += x dlogit^T in registers across tiles; (STATS) the
-//            BN-backward partials of its channel; lanes < (TP / 32) NC: the tile's dlogit column
-//            sums (db), 32 rows each;
+//   phase 2: one lane per (pixel, channel pair): dx = W dlogit with W's two rows in registers,
+//            dW += x dlogit^T in registers across tiles, (STATS) the BN-backward partials of dx;
+//            lanes < 8 NC: the tile's dlogit column sums (db), 32 rows each;
 //   end    : fixed-order LDS reductions -> per-block partials of dW (Cin x ncls), db (ncls) and
 //            (STATS) bnpart[block][0 | 1][c] = sum g | sum g xhat, g = dx [z sc + sh > 0].
-// 128-pixel tiles and class halves keep it at <= 168 VGPRs and 39 KB of LDS: three or more
-// blocks per CU, so one block's staging / phase 1 overlaps another's phase 2 (the 256-pixel,
-// whole-class form ran 2 blocks per CU at 206 VGPRs / 77 KB).
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <int MODE, int NC, int LOSS, bool STATS>
-__global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, int64_t hw, int ncls,
+__global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int64_t hw, int ncls,
                                                          const float* __restrict__ W, const float* __restrict__ prob,
                                                          const float* __restrict__ yt, const float* __restrict__ sums,
                                                          float smooth, float gscale, bool vec, float* __restrict__ dx,
@@ -747,24 +741,18 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
                                                          const float* __restrict__ mu, const float* __restrict__ rs,
                                                          float* __restrict__ bnpart, int ko) {
     main_stream_prio();
-    constexpr int TP = 128;                // pixels a tile
-    constexpr int H = NC >= 8 ? 2 : 1;     // class halves a channel pair
-    constexpr int NH = NC / H;             // classes a lane (a multiple of 4)
     constexpr int LD = NC + 4;
-    __shared__ __attribute__((aligned(16))) float Pt[TP * NC];
-    __shared__ __attribute__((aligned(16))) float Gt[TP * NC];
-    __shared__ __attribute__((aligned(16))) float dls[TP * LD];
-    __shared__ __attribute__((aligned(16))) float4 red[256];
-    const int Cin = v.c0, CP = Cin / 2;    // CP * H divides 256 (launcher)
-    const int kp = threadIdx.x % CP, hh = (threadIdx.x / CP) % H, pp = threadIdx.x / (CP * H);
-    const int PS = 256 / (CP * H);
-    const int c0 = 2 * kp, cl0 = hh * NH;  // channel pair, first class of this lane
-    const int ch = H == 2 ? c0 + hh : c0;  // (H == 2) the channel this lane stores
-    f2v wr[NH], dw[NH];
+    __shared__ __attribute__((aligned(16))) float Pt[256 * NC];
+    __shared__ __attribute__((aligned(16))) float Gt[256 * NC];
+    __shared__ __attribute__((aligned(16))) float dls[256 * LD];
+    const int Cin = v.c0, CP = Cin / 2;
+    const int kp = threadIdx.x % CP, pp = threadIdx.x / CP, PS = 256 / CP;
+    const int c0 = 2 * kp;
+    // the channel pair's kernel rows and weight-gradient sums as float pairs (packed FMAs)
+    f2v wr[NC], dw[NC];
 #pragma unroll
-    for (int c = 0; c < NH; ++c) {
-        const int cc = cl0 + c;
-        wr[c] = cc < ncls ? f2v{W[c0 * ncls + cc], W[(c0 + 1) * ncls + cc]} : f2v{0.f, 0.f};
+    for (int c = 0; c < NC; ++c) {
+        wr[c] = c < ncls ? f2v{W[c0 * ncls + c], W[(c0 + 1) * ncls + c]} : f2v{0.f, 0.f};
         dw[c] = f2v{0.f, 0.f};
     }
     float2 hsc = make_float2(1.f, 1.f), hsh = make_float2(0.f, 0.f), smu = hsh, srs = hsh, s1 = hsh, s2 = hsh;
@@ -778,11 +766,10 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
             srs = *reinterpret_cast<const float2*>(rs + c0);
         }
     }
-    constexpr int DBG = TP / 32;                                 // db: 32-row groups
-    const int dbc = threadIdx.x % NC, dbq = threadIdx.x / NC;    // db: column, row group
+    const int dbc = threadIdx.x % NC, dbq = threadIdx.x / NC;  // db: column, 32-row group
     float dbp = 0.f;
-    for (int64_t m0 = (int64_t)blockIdx.x * TP; m0 < M; m0 += (int64_t)gridDim.x * TP) {
-        const int np = M - m0 < TP ? (int)(M - m0) : TP;
+    for (int64_t m0 = (int64_t)blockIdx.x * 256; m0 < M; m0 += (int64_t)gridDim.x * 256) {
+        const int np = M - m0 < 256 ? (int)(M - m0) : 256;
         const int cnt = np * ncls;
         const float* pg = prob + m0 * ncls;
         const float* yg = yt + m0 * ncls;
@@ -810,7 +797,7 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
             Gt[i] = yg[i];
         }
         __syncthreads();
-        if (threadIdx.x < TP) {
+        {
             const int p = threadIdx.x;
             float dl[NC];
 #pragma unroll
@@ -835,7 +822,7 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
                     make_float4(dl[4 * c4], dl[4 * c4 + 1], dl[4 * c4 + 2], dl[4 * c4 + 3]);
         }
         __syncthreads();
-        if (threadIdx.x < DBG * NC && !(ko & 16)) {
+        if (threadIdx.x < 8 * NC && !(ko & 16)) {
             float t = 0.f;
             for (int q = 0; q < 32; ++q) t += dls[(dbq * 32 + q) * LD + dbc];
             dbp += t;
@@ -859,80 +846,66 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
             if (pb + U * PS < np) zload(pb + U * PS);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int p = pb + u * PS;
-                // (no early exit: every lane of a pair must reach the swap; p >= np lanes idle)
-                const bool live = p < np;
-                const int64_t m = m0 + (live ? p : 0);
-                const float2 zr = zc[u];
-                float2 a = zr;
-                if constexpr (MODE == UNET_VIEW_BNRELU)
-                    a = make_float2(fmaxf(fmaf(zr.x, hsc.x, hsh.x), 0.f), fmaxf(fmaf(zr.y, hsc.y, hsh.y), 0.f));
-                if (!live) a = make_float2(0.f, 0.f);
-                f2v o = {0.f, 0.f};
-                const f2v a2 = {a.x, a.y};
-                const float* dp = &dls[(live ? p : 0) * LD + cl0];
+            const int p = pb + u * PS;
+            if (p >= np) break;
+            const int64_t m = m0 + p;
+            const float2 zr = zc[u];
+            float2 a = zr;
+            if constexpr (MODE == UNET_VIEW_BNRELU)
+                a = make_float2(fmaxf(fmaf(zr.x, hsc.x, hsh.x), 0.f), fmaxf(fmaf(zr.y, hsc.y, hsh.y), 0.f));
+            f2v o = {0.f, 0.f};
+            const f2v a2 = {a.x, a.y};
 #pragma unroll
-                for (int c4 = 0; c4 < ((ko & 32) ? 0 : NH / 4); ++c4) {
-                    const float4 d = *reinterpret_cast<const float4*>(dp + 4 * c4);
-                    const float dv[4] = {d.x, d.y, d.z, d.w};
+            for (int c4 = 0; c4 < ((ko & 32) ? 0 : NC / 4); ++c4) {
+                const float4 d = *reinterpret_cast<const float4*>(&dls[p * LD + 4 * c4]);
+                const float dv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const f2v dd = {dv[i], dv[i]};
-                        o = __builtin_elementwise_fma(wr[4 * c4 + i], dd, o);
-                        dw[4 * c4 + i] = __builtin_elementwise_fma(a2, dd, dw[4 * c4 + i]);
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    const f2v dd = {dv[i], dv[i]};
+                    o = __builtin_elementwise_fma(wr[4 * c4 + i], dd, o);
+                    dw[4 * c4 + i] = __builtin_elementwise_fma(a2, dd, dw[4 * c4 + i]);
                 }
-                float ox = o.x, oy = o.y;
-                if constexpr (H == 2) {  // the other class half: lane ^ CP (CP a power of two)
-                    ox += __shfl_xor(ox, CP, 64);
-                    oy += __shfl_xor(oy, CP, 64);
-                }
-                if (live) {
-                    if constexpr (H == 2) {
-                        if (!(ko & 4)) dx[m * Cin + ch] = hh ? oy : ox;
-                    } else {
-                        if (!(ko & 4)) *reinterpret_cast<float2*>(dx + m * Cin + c0) = make_float2(ox, oy);
-                    }
-                    if constexpr (STATS) {
-                        const float gx = a.x > 0.f ? ox : 0.f, gy = a.y > 0.f ? oy : 0.f;
-                        s1.x += gx;
-                        s1.y += gy;
-                        s2.x = fmaf(gx, (zr.x - smu.x) * srs.x, s2.x);
-                        s2.y = fmaf(gy, (zr.y - smu.y) * srs.y, s2.y);
-                    }
-                }
+            }
+            const float ox = o.x, oy = o.y;
+            if (!(ko & 4)) *reinterpret_cast<float2*>(dx + m * Cin + c0) = make_float2(ox, oy);
+            if constexpr (STATS) {
+                const float gx = a.x > 0.f ? ox : 0.f, gy = a.y > 0.f ? oy : 0.f;
+                s1.x += gx;
+                s1.y += gy;
+                s2.x = fmaf(gx, (zr.x - smu.x) * srs.x, s2.x);
+                s2.y = fmaf(gy, (zr.y - smu.y) * srs.y, s2.y);
+            }
             }
         }
     }
-    // per-block partials, each a fixed-order sum over the block's lanes (pixel groups pp)
-    const int L = CP * H;  // lanes of one pixel group
+    // per-block partials, each a fixed-order sum over the block's lanes
+    float4* red = reinterpret_cast<float4*>(Pt);  // 256 float4 (Pt holds 256 NC >= 1024 floats)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int c4 = 0; c4 < NH / 4; ++c4) {
+        for (int c4 = 0; c4 < NC / 4; ++c4) {
             __syncthreads();
             red[threadIdx.x] = j == 0 ? make_float4(dw[4 * c4].x, dw[4 * c4 + 1].x, dw[4 * c4 + 2].x, dw[4 * c4 + 3].x)
                                       : make_float4(dw[4 * c4].y, dw[4 * c4 + 1].y, dw[4 * c4 + 2].y, dw[4 * c4 + 3].y);
             __syncthreads();
-            if (threadIdx.x < L) {
+            if (threadIdx.x < CP) {
                 float4 t = red[threadIdx.x];
-                for (int q = threadIdx.x + L; q < 256; q += L) t = add4(t, red[q]);
-                const int cc = cl0 + 4 * c4;
-                float* o = part_w + (int64_t)blockIdx.x * Cin * ncls + (c0 + j) * ncls + cc;
-                if (cc + 0 < ncls) o[0] = t.x;
-                if (cc + 1 < ncls) o[1] = t.y;
-                if (cc + 2 < ncls) o[2] = t.z;
-                if (cc + 3 < ncls) o[3] = t.w;
+                for (int q = threadIdx.x + CP; q < 256; q += CP) t = add4(t, red[q]);
+                float* o = part_w + (int64_t)blockIdx.x * Cin * ncls + (2 * threadIdx.x + j) * ncls + 4 * c4;
+                if (4 * c4 + 0 < ncls) o[0] = t.x;
+                if (4 * c4 + 1 < ncls) o[1] = t.y;
+                if (4 * c4 + 2 < ncls) o[2] = t.z;
+                if (4 * c4 + 3 < ncls) o[3] = t.w;
             }
         }
-    if constexpr (STATS) {  // both lanes of a pair accumulated the pair's two channels: take hh == 0
+    if constexpr (STATS) {
         __syncthreads();
         red[threadIdx.x] = make_float4(s1.x, s1.y, s2.x, s2.y);
         __syncthreads();
-        if (threadIdx.x < L && hh == 0) {
+        if (threadIdx.x < CP) {
             float4 t = red[threadIdx.x];
-            for (int q = threadIdx.x + L; q < 256; q += L) t = add4(t, red[q]);
-            float* o = bnpart + (int64_t)blockIdx.x * 2 * Cin + c0;
+            for (int q = threadIdx.x + CP; q < 256; q += CP) t = add4(t, red[q]);
+            float* o = bnpart + (int64_t)blockIdx.x * 2 * Cin + 2 * threadIdx.x;
             o[0] = t.x;
             o[1] = t.y;
             o[Cin] = t.z;
@@ -944,7 +917,7 @@ __global__ __launch_bounds__(256, 3) void head_bwdmf_kernel(DView v, int64_t M, 
     __syncthreads();
     if (threadIdx.x < ncls) {
         float t = 0.f;
-        for (int q = 0; q < DBG; ++q) t += Gt[q * NC + threadIdx.x];
+        for (int q = 0; q < 8; ++q) t += Gt[q * NC + threadIdx.x];
         part_b[(int64_t)blockIdx.x * ncls + threadIdx.x] = t;
     }
 }
@@ -1180,13 +1153,12 @@ int head_bwd_grid(int64_t M) {
     return (int)(g > 1024 ? 1024 : g);
 }
 // the fused multi-class backward (head_bwdmf_kernel) covers this head
-bool head_bwdmf_ok(const unet_view* x, int ncls) {  // (Cin / 2) x class halves divides 256
-    const int halves = ncls > 4 ? 2 : 1;
-    return ncls > 1 && ncls <= 24 && x->c0 <= 64 && x->c0 % 4 == 0 && 256 % (x->c0 / 2 * halves) == 0;
+bool head_bwdmf_ok(const unet_view* x, int ncls) {
+    return ncls > 1 && ncls <= 24 && x->c0 <= 64 && x->c0 % 4 == 0 && 256 % (x->c0 / 2) == 0;
 }
-int head_bwdmf_grid(int64_t M) {  // 128-pixel tiles, up to 4 blocks a CU: one wave of blocks
-    const int64_t g = cdiv(M, 128);
-    return (int)(g > 1024 ? 1024 : g);
+int head_bwdmf_grid(int64_t M) {  // 2 blocks a CU (77 KB of LDS at 24 classes): one wave of blocks
+    const int64_t g = cdiv(M, 256);
+    return (int)(g > 512 ? 512 : g);
 }
 int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float* kernel, const float* prob,
                   const float* y_true, const float* sums, float smooth, int loss_kind, float loss_scale, float* dx,
