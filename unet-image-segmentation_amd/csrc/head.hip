@@ -227,10 +227,9 @@ __global__ __launch_bounds__(256) void dice_partial_m_kernel(const float* __rest
     }
 }
 
-// One wave per (image, class) term (the 4 waves take terms w, w + 4, ...): lane b sums the block
-// partials b, b + 64, ... in double, an xor-shuffle tree (fixed lane order) combines the lanes;
-// the dice / iou terms are then added in term order by thread 0 -- deterministic, and no thread
-// walks all nblk partials serially.
+// Per (image, class) term: the block partials summed in double by a group of lanes and an
+// xor-shuffle tree (fixed lane order); the dice / iou terms then summed by one wave in a fixed
+// order -- deterministic, and no thread walks all nblk partials or all terms serially.
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -264,21 +263,31 @@ __global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* part, 
         part = pst;
     }
     if (threadIdx.x == 0) acc[0] = acc[1] = 0.0;
+    // 8 lanes a term (lane g sums partials g, g + 8, ... in double, then an xor tree within the
+    // group): 128 terms at a time instead of one a wave; the terms' dice / iou values are then
+    // summed by one wave (lane t: terms t, t + 64, ..., then its xor tree) -- fixed orders both
+    constexpr int G = 8;
+    const int grp = threadIdx.x / G, gl = threadIdx.x % G, ngrp = (int)(blockDim.x / G);
     for (int base = 0; base < N * ncls; base += kMaxTerms) {
         const int nt = N * ncls - base < kMaxTerms ? N * ncls - base : kMaxTerms;
-        for (int k = wave; k < nt; k += (int)(blockDim.x >> 6)) {
-            const int idx = base + k, n = idx / ncls, c = idx % ncls;
+        for (int k0 = 0; k0 < nt; k0 += ngrp) {  // (uniform trip count: the shuffles see every lane)
+            const int k = k0 + grp;
+            const int idx = base + (k < nt ? k : 0), n = idx / ncls, c = idx % ncls;
             double I = 0.0, T = 0.0, P = 0.0;
-            for (int b = lane; b < nblk; b += 64) {
-                const int64_t o = (((int64_t)n * nblk + b) * 3) * ncls + c;
-                I += part[o];
-                T += part[o + ncls];
-                P += part[o + 2 * ncls];
+            if (k < nt)
+                for (int b = gl; b < nblk; b += G) {
+                    const int64_t o = (((int64_t)n * nblk + b) * 3) * ncls + c;
+                    I += part[o];
+                    T += part[o + ncls];
+                    P += part[o + 2 * ncls];
+                }
+#pragma unroll
+            for (int o = G / 2; o > 0; o >>= 1) {
+                I += __shfl_xor(I, o, 64);
+                T += __shfl_xor(T, o, 64);
+                P += __shfl_xor(P, o, 64);
             }
-            I = wave_sum_d(I);
-            T = wave_sum_d(T);
-            P = wave_sum_d(P);
-            if (lane == 0) {
+            if (gl == 0 && k < nt) {
                 const float fi = (float)I, ft = (float)T, fp = (float)P;
                 if (sums) {
                     sums[idx * 3 + 0] = fi;
@@ -290,14 +299,18 @@ __global__ __launch_bounds__(1024) void dice_finalize_kernel(const float* part, 
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            double d = acc[0], i = acc[1];
-            for (int k = 0; k < nt; ++k) {
+        if (wave == 0) {
+            double d = 0.0, i = 0.0;
+            for (int k = lane; k < nt; k += 64) {
                 d += (double)td[k];
                 i += (double)ti[k];
             }
-            acc[0] = d;
-            acc[1] = i;
+            d = wave_sum_d(d);
+            i = wave_sum_d(i);
+            if (lane == 0) {
+                acc[0] += d;
+                acc[1] += i;
+            }
         }
         __syncthreads();
     }
@@ -745,6 +758,8 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
     __shared__ __attribute__((aligned(16))) float Pt[256 * NC];
     __shared__ __attribute__((aligned(16))) float Gt[256 * NC];
     __shared__ __attribute__((aligned(16))) float dls[256 * LD];
+    __shared__ float cf[2 * NC * 3];  // the tile's per-(image, class) dice sums (hw >= 256: <= 2 images)
+    const bool cfl = hw >= 256;
     const int Cin = v.c0, CP = Cin / 2;
     const int kp = threadIdx.x % CP, pp = threadIdx.x / CP, PS = 256 / CP;
     const int c0 = 2 * kp;
@@ -796,6 +811,11 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
             Pt[i] = pg[i];
             Gt[i] = yg[i];
         }
+        const int64_t n0 = m0 / hw;
+        if (cfl && threadIdx.x < 2 * ncls * 3) {
+            const int64_t o = n0 * ncls * 3 + threadIdx.x;
+            cf[threadIdx.x] = o < (M / hw) * ncls * 3 ? sums[o] : 0.f;
+        }
         __syncthreads();
         {
             const int p = threadIdx.x;
@@ -803,7 +823,8 @@ __global__ __launch_bounds__(256) void head_bwdmf_kernel(DView v, int64_t M, int
 #pragma unroll
             for (int c = 0; c < NC; ++c) dl[c] = 0.f;
             if (p < np && !(ko & 64)) {
-                const float* s3 = sums + ((m0 + p) / hw) * ncls * 3;
+                const int64_t nimg = (m0 + p) / hw;
+                const float* s3 = cfl ? cf + (nimg - n0) * ncls * 3 : sums + nimg * ncls * 3;
                 float s = 0.f;
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
