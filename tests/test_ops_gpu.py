@@ -374,12 +374,16 @@ def test_head_dice(ops, ncls, loss_kind):
 
 
 @pytest.mark.parametrize("ncls", [2, 3, 8, 21, 32])
-@pytest.mark.parametrize("cin,mode,nhw", [(64, 1, (3, 64, 40)), (16, 0, (2, 13, 11)), (48, 1, (1, 17, 19)),
-                                          (128, 1, (1, 9, 7)), (4, 1, (1, 300, 1))])
-def test_head_multiclass_shapes(ops, ncls, cin, mode, nhw):
+@pytest.mark.parametrize("cin,mode,nhw,unaligned", [(64, 1, (3, 64, 40), False), (16, 0, (2, 13, 11), False),
+                                                    (48, 1, (1, 17, 19), False), (128, 1, (1, 9, 7), False),
+                                                    (4, 1, (1, 300, 1), False), (64, 1, (2, 17, 19), False),
+                                                    (64, 1, (2, 17, 19), True)])
+def test_head_multiclass_shapes(ops, ncls, cin, mode, nhw, unaligned):
     """Softmax head forward + dice-loss backward (u_net.py:105-112, losses) over class counts that
-    round up to every register width (4..32), ragged and multi-tile pixel counts, the register
-    kernels (Cin <= 64, Cin/4 dividing 256) and the general ones (Cin 48 backward, Cin 128)."""
+    round up to every register width (4..32), ragged and multi-tile pixel counts, tiles that span
+    two images (323 pixels an image), the register kernels (Cin <= 64, Cin/4 dividing 256) and the
+    general ones (Cin 48 backward, Cin 128); unaligned: prob and y_true start 4 bytes past a
+    16-byte boundary (the scalar staging / store paths)."""
     n, h, w = nhw
     rng = np.random.default_rng(ncls * 131 + cin)
     a, t = _view_inputs(rng, mode, n, h, w, cin)
@@ -387,18 +391,28 @@ def test_head_multiclass_shapes(ops, ncls, cin, mode, nhw):
     xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"))
     k = f32(rng.standard_normal((1, 1, cin, ncls)) * 0.2)
     b = f32(rng.standard_normal(ncls) * 0.1)
-    prob = torch.full((n, h, w, ncls), -1.0, device="cuda")
+
+    def buf(arr=None):
+        size = n * h * w * ncls
+        base = torch.full((size + 1,), -1.0, device="cuda")
+        out = base[1:] if unaligned else base[:size]
+        if arr is not None:
+            out.copy_(torch.from_numpy(np.ascontiguousarray(arr, dtype=np.float32).reshape(-1)))
+        return out.view(n, h, w, ncls)
+    prob = buf()
     ops.head_fwd(v, n, h, w, ncls, dev(k), dev(b), prob)
     pp = host(prob)
     assert rel_err(pp, K.head(xv, k, b, ncls)) < 2e-6
     yt = np.eye(ncls)[rng.integers(0, ncls, (n, h, w))]
+    ytd = buf(yt)
     sums = torch.empty(n * ncls * 3, device="cuda")
     res = torch.empty(3, device="cuda")
-    ops.dice_fwd(dev(yt), prob, n, h * w, ncls, 1e-7, sums, res)
+    ops.dice_fwd(ytd, prob, n, h * w, ncls, 1e-7, sums, res)
+    assert abs(host(res)[0] - K.dice_loss(yt, pp)) < 1e-6
     dx = torch.full((n, h, w, cin), 7.0, device="cuda")
     dk = torch.empty((1, 1, cin, ncls), device="cuda")
     db = torch.empty(ncls, device="cuda")
-    ops.head_bwd(v, n, h, w, ncls, dev(k), prob, dev(yt), sums, 1e-7, 0, dx, dk, db)
+    ops.head_bwd(v, n, h, w, ncls, dev(k), prob, ytd, sums, 1e-7, 0, dx, dk, db)
     rdx, rdk, rdb = K.head_bwd(xv, k, pp, K.dice_loss_grad(yt, pp), ncls)
     assert rel_err(host(dx), rdx) < 1e-4
     assert rel_err(host(dk), rdk) < 1e-4
