@@ -191,10 +191,12 @@ int unet_pool_select(const float* z, int n, int h, int w, int c, const float* ga
  * (max-pool views of > 128 outputs: its 256-wide tile pools each halo element once for all
  * columns).  TILE / RK force one (RK fails with -1 where it does not exist): both are
  * parity-tested (tests/test_ops_gpu.py).  With pw_kernel_x3, 64 / 128 input and output channels and
- * a plain / BN+ReLU / concat view, AUTO and RK run the register-A kernel PERSISTENT over pixel
- * tiles (sepconv_px.hip: a block walks a run of tiles as one stream of k-stages, the next stages'
- * loads in flight across tile boundaries); RK1 forces the one-tile-per-block register-A kernel
- * (same products, same per-tile statistics partials up to the order of the 4-wave combine).
+ * a plain / BN+ReLU / concat view, RK runs the register-A kernel PERSISTENT over pixel tiles
+ * (sepconv_px.hip: a block walks a run of tiles as one stream of k-stages, the next stages' loads
+ * in flight across tile boundaries); AUTO does so only where that measured faster inside the train
+ * step (128 outputs from 64 inputs or with z_pool_sel); RK1 forces the one-tile-per-block
+ * register-A kernel (same products, same per-tile statistics partials up to the order of the
+ * 4-wave combine).
  * Without pw_kernel_x3 the results are identical: both
  * form each output as the same k-ordered fmaf chain.  With pw_kernel_x3 the register-A kernel
  * runs its split-precision (bf16x6 MFMA) variant, whose summation order differs (results within

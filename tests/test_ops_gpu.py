@@ -935,14 +935,14 @@ PX_CASES = [
     (0, 2, 64, 64, 128, 0, 64, 0.0, False, True),     # plain view, 128 -> 64, inference epilogue
     (1, 4, 128, 128, 128, 0, 128, 0.0, True, True),   # enc2_block2's shape at batch 4
     (3, 2, 256, 256, 64, 64, 64, 0.0, True, False),   # dec1_block1's shape at batch 2
-    (1, 2, 256, 256, 64, 0, 64, 0.0, True, True),     # enc1_block2 (64 -> 64: the one-tile kernel in both)
+    (1, 2, 256, 256, 64, 0, 64, 0.0, True, True),     # enc1_block2's shape (64 -> 64)
 ]
 
 
 @pytest.mark.parametrize("mode,n,h,w,c0,c1,cout,drop,train,zsel", PX_CASES)
 def test_sepconv_persistent_matches_one_tile(ops, mode, n, h, w, c0, c1, cout, drop, train, zsel):
-    """The persistent split-precision forward (sepconv_px.hip, schedule AUTO / RK) against the
-    one-tile-per-block register-A kernel (schedule RK1) with the same split planes: the same
+    """The persistent split-precision forward (sepconv_px.hip, schedule RK: every supported shape)
+    against the one-tile-per-block register-A kernel (schedule RK1) with the same split planes: the same
     products in the same order, so z, y and the pooling selection are bitwise equal; the per-tile
     BN partials combine the four waves' 32-row moments by Chan's formula instead of a two-pass sum
     over 128 rows (fp32 rounding apart).  Also against the float64 oracle."""
@@ -958,7 +958,7 @@ def test_sepconv_persistent_matches_one_tile(ops, mode, n, h, w, c0, c1, cout, d
     v = _mk_view(ops, mode, t, drop, 31)
     m = n * h * w
     outs = []
-    for sch in (ops.SEPCONV_RK1, ops.SEPCONV_AUTO):
+    for sch in (ops.SEPCONV_RK1, ops.SEPCONV_RK):
         old = ops.sepconv_set_schedule(sch)
         try:
             y = torch.full((n, h, w, C), -7.0, device="cuda") if train else None

@@ -1,5 +1,5 @@
 """Lab: the persistent split-precision sepconv forward (sepconv_px.hip, schedule AUTO) against the
-one-tile-per-block register-A kernel (schedule RK1) on the short-K shapes: z / y / pooling
+one-tile-per-block register-A kernel (schedule RK1) on the short-K shapes (schedule RK: every supported shape): z / y / pooling
 selection compared (bitwise expected: same products, same order) and the BN statistics partials
 (per tile, combined in a different order: ~1e-6 relative), and both timed with HIP events around
 back-to-back launches (median of 3 groups of 10).  With the lab library (UNET_HIP_LIB=
@@ -59,7 +59,7 @@ def run_shape(name, mode, n, hw, cc, cout, wy, sel, drop, stats):
     m = n * hw * hw
     gam = rnd(cout) if sel else None
     outs = {}
-    for sch in (ops.SEPCONV_RK1, ops.SEPCONV_AUTO):
+    for sch in (ops.SEPCONV_RK1, ops.SEPCONV_RK):
         y = torch.full((n, hw, hw, cin), float("nan"), device=dev) if wy else None
         z = torch.full((n, hw, hw, cout), float("nan"), device=dev)
         part = torch.zeros(ops.bn_partials_numel(m, cout), device=dev) if stats else None
@@ -85,7 +85,7 @@ def run_shape(name, mode, n, hw, cc, cout, wy, sel, drop, stats):
             rec["us"] = sorted(ts)[1]
         ops.sepconv_set_schedule(old)
         outs[sch] = rec
-    a, b = outs[ops.SEPCONV_RK1], outs[ops.SEPCONV_AUTO]
+    a, b = outs[ops.SEPCONV_RK1], outs[ops.SEPCONV_RK]
     res = {"shape": name, "n": n, "hw": hw, "cin": cin, "cout": cout}
     res["z_bitwise"] = bool(torch.equal(a["z"], b["z"]))
     res["z_maxrel"] = float(((a["z"] - b["z"]).abs().max() / a["z"].abs().max()).item())

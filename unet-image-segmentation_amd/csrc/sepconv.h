@@ -40,7 +40,7 @@ bool rk_x6_supported(int mode, int cin);
 bool rk_supported(int mode, int cin, int cout);
 // persistent split-precision schedule (sepconv_px.hip) for 64 / 128 input and output channels:
 // returns 0, or -1 if the shape has no such kernel (needs a.pkx)
-bool px_supported(const SepArgs& a, int mode);
+bool px_supported(const SepArgs& a, int mode, bool all_shapes);
 int launch_px(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st);
 
 }  // namespace sep

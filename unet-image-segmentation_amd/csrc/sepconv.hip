@@ -474,7 +474,7 @@ extern "C" int unet_sepconv_fwd(const unet_view* x, int n, int h, int w, const f
     if (g_sep_schedule != UNET_SEPCONV_TILE && rk_supported(x->mode, a.Cin, cout)) {
         // the persistent split-precision kernel for the short-K shapes (sepconv_px.hip), unless
         // the one-tile-per-block register-A kernel is forced
-        if (g_sep_schedule != UNET_SEPCONV_RK1 && px_supported(a, x->mode)) {
+        if (g_sep_schedule != UNET_SEPCONV_RK1 && px_supported(a, x->mode, g_sep_schedule == UNET_SEPCONV_RK)) {
             if (launch_px(a, x->mode, drop, stats, wy, st)) return -1;
             UNET_CHECK_LAUNCH("unet_sepconv_fwd");
             return 0;

@@ -401,20 +401,23 @@ void launch_px_m(const SepArgs& a, bool stats, bool write_y, int pd, int ntiles,
 
 }  // namespace
 
-bool px_supported(const SepArgs& a, int mode) {
-    if (!a.pkx) return false;
+bool px_supported(const SepArgs& a, int mode, bool all_shapes) {
+    if (!a.pkx || lab_knob("UNET_PX", 1) == 0) return false;  // (lab: UNET_PX=0 keeps the one-tile kernel)
     if (mode != UNET_VIEW_PLAIN && mode != UNET_VIEW_BNRELU && mode != UNET_VIEW_CONCAT) return false;
     if ((a.Cin != 64 && a.Cin != 128) || (a.Cout != 64 && a.Cout != 128)) return false;
-    // 64 -> 64 too since the epilogue stopped draining the prefetch (gamma signs read once):
-    // enc1_block2 1.09x, dec1_block2 1.14x the one-tile kernel (profiles/r4l_px_lab.log; it was
-    // 0.96x before, r4b).  UNET_PX_6464=0 (lab) keeps 64 -> 64 on the one-tile kernel.
-    if (a.Cin == 64 && a.Cout == 64 && lab_knob("UNET_PX_6464", 1) == 0) return false;
+    // Only the shapes where it wins INSIDE the train step: 128 outputs from 64 inputs or with the
+    // pool-selection epilogue (enc2_block1 79.0 -> 78.2 us, enc2_block2 147.2 -> 138.8 us).  Isolated
+    // on a repeated input it also beats the one-tile kernel on 64 -> 64 (1.09-1.14x,
+    // profiles/r4l_px_lab.log), but in the step enc1_block2 165 -> 173, dec1_block2 137 -> 158,
+    // dec1_block1 258 -> 265, dec2_block2 133 -> 136 us (profiles/r4q_px_in_step.txt).
+    // all_shapes (schedule RK) or UNET_PX_ALL=1 (lab) take every supported shape.
+    if (!all_shapes && lab_knob("UNET_PX_ALL", 0) == 0 && !(a.Cout == 128 && (a.Cin == 64 || a.zsel))) return false;
     if (mode == UNET_VIEW_CONCAT && a.x.c0 % 16) return false;
     return a.H % TH == 0 && a.W % TW == 0;
 }
 
 int launch_px(const SepArgs& a, int mode, bool drop, bool stats, bool write_y, hipStream_t st) {
-    if (!px_supported(a, mode)) return -1;
+    if (!px_supported(a, mode, true)) return -1;
     const int ntiles = a.N * (a.H / TH) * (a.W / TW);
     // two blocks per CU; equal runs of tiles (the grid is the tile count / the tiles per block)
     const int slots = 256 * lab_knob("UNET_PX_BPC", 2);
