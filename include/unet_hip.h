@@ -325,6 +325,26 @@ int unet_pointwise_bwd_data_bnrelu_wgrad(const float* da, const float* z,
                                          void* ws, size_t ws_bytes,
                                          unet_stream_t stream);
 
+/* The image block's two weight gradients in ONE streaming pass (its data gradient is
+ * never needed): as unet_pointwise_bwd_data_bnrelu_wgrad, but the dy it forms per
+ * pixel is not stored, it is contracted at once with the pixel's 3x3 neighbourhood
+ * of x into the depthwise kernel gradient.  x: the (n, h, w, 4) input the forward
+ * read (channels past wcin zero), pw_kernel (4, cout) padded the same way.  Outputs
+ * in the Keras shapes of the wcin-channel layer: d_dw_kernel (3, 3, wcin, 1),
+ * d_pw_kernel (1, 1, wcin, cout) -- both overwritten.  cout 32 or 64.
+ * Replaces the backward of the first SeparableConv2D (model/u_net.py:14-20 for
+ * the first conv_block, u_net.py:62) for its weights.
+ * Workspace: _workspace(n, h, w, cout) bytes (0: shape not supported).       */
+size_t unet_image_block_bwd_wgrad_workspace(int n, int h, int w, int cout);
+int unet_image_block_bwd_wgrad(const float* x, int n, int h, int w, int wcin,
+                               int cout, const float* pw_kernel,
+                               const float* scale, const float* shift,
+                               const float* coef, const float* da,
+                               const float* z, const float* y,
+                               float* d_dw_kernel, float* d_pw_kernel,
+                               void* ws, size_t ws_bytes,
+                               unet_stream_t stream);
+
 /* ----- Conv2DTranspose(f, 2, strides=2, padding='same') — u_net.py:88-94 --
  * out[n, 2i+a, 2j+b, co] = bias[co] + sum_ci x[n,i,j,ci] * k[a,b,co,ci];
  * kernel is Keras (2, 2, Cout, Cin), x a view of (n, h, w, Cin).           */

@@ -245,6 +245,47 @@ def test_pointwise_bwd_data_bnrelu_wgrad(ops, use_bn, m, cout):
     assert not torch.any(dpk_f[0, 0, 3])  # zero input channel -> zero gradient row
 
 
+@pytest.mark.parametrize("cout", [32, 64])
+@pytest.mark.parametrize("n,h,w,wcin", [(2, 17, 19, 3), (1, 64, 64, 3), (3, 8, 5, 4), (1, 3, 130, 3)])
+def test_image_block_bwd_wgrad(ops, n, h, w, wcin, cout):
+    """Both image-block weight gradients in one pass (dy formed and contracted with x's 3x3
+    neighbourhood, never stored), in the Keras wcin-channel shapes: against the two-launch path
+    (data + pointwise gradient, then the depthwise filter gradient over the stored dy) and the
+    float64 restatement of dK[i, j, c] = sum dy[p, c] x[p + (i - 1, j - 1), c] (zero padding)."""
+    rng = np.random.default_rng(n * 1000 + h * 10 + w + cout + wcin)
+    m, cin, c = n * h * w, 4, cout
+    x = f32(rng.standard_normal((n, h, w, cin)))
+    x[..., wcin:] = 0.0
+    z = f32(rng.standard_normal((m, c)) * 2 + 0.3)
+    da = f32(rng.standard_normal((m, c)))
+    y = f32(rng.standard_normal((m, cin)))
+    y[:, wcin:] = 0.0
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cout))
+    pk[:, :, wcin:] = 0.0
+    gamma, beta = bn_affine(rng, c)
+    mean, var = z.mean(0), z.var(0)
+    rstd = 1 / np.sqrt(var + 1e-3)
+    ts, th = dev(f32(gamma * rstd)), dev(f32(beta - mean * gamma * rstd))
+    dg, db, coef = torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda"), torch.empty(3 * c, device="cuda")
+    ops.bn_relu_bwd_stats(dev(da), dev(z), m, c, dev(f32(mean)), dev(f32(rstd)), ts, th, True, 0.0, 0, dg, db, coef)
+    ddk = torch.full((3, 3, wcin, 1), 7.0, device="cuda")
+    dpk = torch.full((1, 1, wcin, cout), 7.0, device="cuda")
+    tx = dev(x)
+    ops.image_block_bwd_wgrad(tx, n, h, w, wcin, cout, dev(pk), ts, th, coef, dev(da), dev(z), dev(y), ddk, dpk)
+    assert ops.L.query("unet_image_block_bwd_wgrad_workspace", n, h, w, 48) == 0
+    dy = torch.empty((m, cin), device="cuda")
+    dpk_p = torch.empty((1, 1, cin, cout), device="cuda")
+    ops.pointwise_bwd_data_bnrelu_wgrad(dev(da), dev(z), m, cin, cout, dev(pk), ts, th, coef, dev(y), dy, dpk_p)
+    assert rel_err(host(dpk), host(dpk_p)[:, :, :wcin]) < 1e-5
+    ddk_p = torch.empty((3, 3, cin, 1), device="cuda")
+    ops.dwconv3x3_bwd_filter(ops.View.plain(tx), n, h, w, dy, ddk_p)
+    assert rel_err(host(ddk), host(ddk_p)[:, :, :wcin]) < 1e-5
+    g = host(dy).astype(np.float64).reshape(n, h, w, cin)
+    xp = np.pad(x.astype(np.float64), ((0, 0), (1, 1), (1, 1), (0, 0)))
+    ref = np.stack([np.stack([(g * xp[:, i:i + h, j:j + w]).sum((0, 1, 2)) for j in range(3)]) for i in range(3)])
+    assert rel_err(host(ddk)[..., 0], ref[..., :wcin]) < 1e-5
+
+
 @pytest.mark.parametrize("use_bn,drop", [(True, 0.0), (True, 0.2), (False, 0.0)])
 @pytest.mark.parametrize("m,cin,cout", [(300, 16, 32), (1000, 64, 128), (257, 128, 64), (128, 4, 8),
                                        (520, 1024, 64)])  # cin >= 1024: dz pass + plain GEMM

@@ -1134,15 +1134,28 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
 // per pixel (one channel quad each), U pixels in flight per lane; dy by xor shuffles over the G
 // lanes, dW accumulated per lane over its pixels, then over the lanes / waves of the block into
 // one slab per block.
-template <int G>
+//
+// DWF (unet_image_block_bwd_wgrad): the depthwise kernel gradient too.  dy is not stored: it only
+// feeds dK[tap][c] = sum_p dy[p, c] x[p + tap offset, c], so once the xor butterfly has given all
+// G lanes of a pixel its dy, lane q accumulates taps q and q + G (< 9) against the pixel's
+// neighbours in x, loaded beside da / z / y at the top of the iteration (zero outside the image
+// and past M).  Slab = [4][C] pointwise | [9][4] depthwise (SW floats).
+template <int G, bool DWF = false>
 __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict__ da, const float* __restrict__ z,
                                                          int64_t M, const float* __restrict__ P,
                                                          const float* __restrict__ sc, const float* __restrict__ sh,
                                                          const float* __restrict__ coef, const float* __restrict__ y,
-                                                         float* __restrict__ dy, float* __restrict__ wpart) {
+                                                         float* __restrict__ dy, float* __restrict__ wpart,
+                                                         const float* __restrict__ x = nullptr, int H = 0, int W = 0) {
     main_stream_prio();
     constexpr int C = 4 * G, PPW = 64 / G, U = 4, PB = 4 * U * PPW;
+    constexpr int NT = DWF ? (9 + G - 1) / G : 0;  // taps per lane
+    constexpr int SW = 4 * C + (DWF ? 36 : 0);   // slab width
     __shared__ float4 red[4][4][G];  // [wave][ci][quad]
+    __shared__ float4 rdk[4][DWF ? 9 : 1];  // [wave][tap]
+    float4 gacc[NT > 0 ? NT : 1];
+#pragma unroll
+    for (int i = 0; i < (NT > 0 ? NT : 1); ++i) gacc[i] = f4(0.f);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int q = lane % G, ps = lane / G;
     const int c = 4 * q;
@@ -1157,6 +1170,7 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
     for (int64_t base = (int64_t)blockIdx.x * PB; base < M; base += (int64_t)gridDim.x * PB) {
         const int64_t p0 = base + wave * U * PPW + ps;
         float4 ra[U], rz[U], ry[U];
+        float4 xn[U][NT > 0 ? NT : 1];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t m = p0 + u * PPW;
@@ -1164,6 +1178,17 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
             ra[u] = in ? ld4(da + m * C + c) : f4(0.f);
             rz[u] = in ? ld4(z + m * C + c) : f4(0.f);
             ry[u] = in ? ld4(y + m * 4) : f4(0.f);
+            if constexpr (DWF) {
+                const int mi = in ? (int)m : 0;  // M * C fits int32 (checked on the host)
+                const int hw = H * W;
+                const int r = mi - (mi / hw) * hw, hh = r / W, ww = r - hh * W;
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const int t = q + i * G, di = t / 3 - 1, dj = t % 3 - 1;
+                    const bool ok = in && t < 9 && hh + di >= 0 && hh + di < H && ww + dj >= 0 && ww + dj < W;
+                    xn[u][i] = ok ? ld4(x + (int64_t)(mi + di * W + dj) * 4) : f4(0.f);
+                }
+            }
         }
         float4 s[U];
 #pragma unroll
@@ -1197,7 +1222,12 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
                 s[u].z += __shfl_xor(s[u].z, off, 64);
                 s[u].w += __shfl_xor(s[u].w, off, 64);
             }
-        if (q == 0) {
+        if constexpr (DWF) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int i = 0; i < NT; ++i) gacc[i] = fma4(xn[u][i], s[u], gacc[i]);
+        } else if (q == 0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t m = p0 + u * PPW;
@@ -1215,6 +1245,22 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
             wacc[ci].z += __shfl_xor(wacc[ci].z, off, 64);
             wacc[ci].w += __shfl_xor(wacc[ci].w, off, 64);
         }
+    if constexpr (DWF) {
+#pragma unroll
+        for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                gacc[i].x += __shfl_xor(gacc[i].x, off, 64);
+                gacc[i].y += __shfl_xor(gacc[i].y, off, 64);
+                gacc[i].z += __shfl_xor(gacc[i].z, off, 64);
+                gacc[i].w += __shfl_xor(gacc[i].w, off, 64);
+            }
+        if (lane < G) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (lane + i * G < 9) rdk[wave][lane + i * G] = gacc[i];
+        }
+    }
     if (lane < G) {
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci) red[wave][ci][lane] = wacc[ci];
@@ -1223,11 +1269,37 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
     if (threadIdx.x < 4 * G) {
         const int ci = threadIdx.x / G, qq = threadIdx.x % G;
         const float4 t = add4(add4(red[0][ci][qq], red[1][ci][qq]), add4(red[2][ci][qq], red[3][ci][qq]));
-        st4(wpart + (int64_t)blockIdx.x * 4 * C + ci * C + 4 * qq, t);
+        st4(wpart + (int64_t)blockIdx.x * SW + ci * C + 4 * qq, t);
+    }
+    if constexpr (DWF) {
+        if (threadIdx.x >= 64 && threadIdx.x < 64 + 9) {
+            const int t = threadIdx.x - 64;
+            const float4 v = add4(add4(rdk[0][t], rdk[1][t]), add4(rdk[2][t], rdk[3][t]));
+            st4(wpart + (int64_t)blockIdx.x * SW + 4 * C + 4 * t, v);
+        }
     }
     if (blockIdx.x == gridDim.x - 1) {  // zero slabs up to a multiple of 64 (the two-level reduction)
         const int S = gridDim.x, Sp = (S + 63) / 64 * 64;
-        for (int i = threadIdx.x; i < (Sp - S) * 4 * C; i += 256) wpart[(int64_t)S * 4 * C + i] = 0.f;
+        for (int i = threadIdx.x; i < (Sp - S) * SW; i += 256) wpart[(int64_t)S * SW + i] = 0.f;
+    }
+}
+
+// Last level of the image block's weight gradients: T rows of the [4][C] | [9][4] slab summed in
+// order (double) and written in the Keras shapes of the 3-channel (wcin) input -- pointwise
+// (1, 1, wcin, C), depthwise (3, 3, wcin, 1) -- so no strided copy follows.
+__global__ __launch_bounds__(256) void img_wgrad_final_kernel(const float* __restrict__ mid, int T, int C, int wcin,
+                                                              float* __restrict__ dpk, float* __restrict__ ddk) {
+    const int SW = 4 * C + 36;
+    for (int l = threadIdx.x; l < SW; l += 256) {
+        double a = 0.0;
+        for (int t = 0; t < T; ++t) a += (double)mid[(int64_t)t * SW + l];
+        if (l < 4 * C) {
+            const int ci = l / C, co = l - ci * C;
+            if (ci < wcin) dpk[ci * C + co] = (float)a;
+        } else {
+            const int tap = (l - 4 * C) >> 2, ch = (l - 4 * C) & 3;
+            if (ch < wcin) ddk[tap * wcin + ch] = (float)a;
+        }
     }
 }
 
@@ -1606,6 +1678,48 @@ extern "C" int unet_pointwise_bwd_data_bnrelu_wgrad(const float* da, const float
     int rc = reduce_slabs(part, 64, T * L, mid, T * L, T * L, st);
     if (rc) return rc;
     return reduce_slabs(mid, (int)T, L, d_pw_kernel, L, L, st);
+}
+
+extern "C" size_t unet_image_block_bwd_wgrad_workspace(int n, int h, int w, int cout) {
+    const int64_t m = (int64_t)n * h * w;
+    if (m <= 0 || (cout != 32 && cout != 64)) return 0;
+    const int64_t sp = cdiv(img_pw_slabs(m, cout), 64) * 64, L = 4 * cout + 36;
+    return align_up((size_t)sp * L * sizeof(float), 256) + align_up((size_t)(sp / 64) * L * sizeof(float), 256);
+}
+
+extern "C" int unet_image_block_bwd_wgrad(const float* x, int n, int h, int w, int wcin, int cout,
+                                          const float* pw_kernel, const float* scale, const float* shift,
+                                          const float* coef, const float* da, const float* z, const float* y,
+                                          float* d_dw_kernel, float* d_pw_kernel, void* ws, size_t ws_bytes,
+                                          unet_stream_t stream) {
+    UNET_CHECK_ARG(x && pw_kernel && scale && shift && coef && da && z && y && d_dw_kernel && d_pw_kernel,
+                   "unet_image_block_bwd_wgrad: null pointer");
+    UNET_CHECK_ARG(n > 0 && h > 0 && w > 0 && wcin >= 1 && wcin <= 4 && (cout == 32 || cout == 64),
+                   "unet_image_block_bwd_wgrad: needs n, h, w > 0, 1 <= wcin <= 4 and cout 32 or 64");
+    const int64_t m = (int64_t)n * h * w;
+    UNET_CHECK_ARG(fits_i32(m, cout), "unet_image_block_bwd_wgrad: tensor too large");
+    UNET_CHECK_ARG(((uintptr_t)x | (uintptr_t)da | (uintptr_t)z | (uintptr_t)coef | (uintptr_t)scale |
+                    (uintptr_t)shift | (uintptr_t)y | (uintptr_t)pw_kernel | (uintptr_t)ws) % 16 == 0,
+                   "unet_image_block_bwd_wgrad: operands must be 16-B aligned");
+    const size_t need = unet_image_block_bwd_wgrad_workspace(n, h, w, cout);
+    UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_image_block_bwd_wgrad: workspace %zu < %zu", ws_bytes, need);
+    hipStream_t st = as_stream(stream);
+    const int S = img_pw_slabs(m, cout);
+    float* part = static_cast<float*>(ws);
+    if (cout == 64)
+        img_pw_bwd_kernel<16, true><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, nullptr, part, x,
+                                                       h, w);
+    else
+        img_pw_bwd_kernel<8, true><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, nullptr, part, x,
+                                                      h, w);
+    UNET_CHECK_LAUNCH("unet_image_block_bwd_wgrad");
+    const int64_t L = (int64_t)4 * cout + 36, sp = cdiv(S, 64) * 64, T = sp / 64;
+    float* mid = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)sp * L * sizeof(float), 256));
+    int rc = reduce_slabs(part, 64, T * L, mid, T * L, T * L, st);
+    if (rc) return rc;
+    img_wgrad_final_kernel<<<1, 256, 0, st>>>(mid, (int)T, cout, wcin, d_pw_kernel, d_dw_kernel);
+    UNET_CHECK_LAUNCH("unet_image_block_bwd_wgrad(final)");
+    return 0;
 }
 
 extern "C" size_t unet_pointwise_bwd_filter_workspace(int64_t m, int cin, int cout) {

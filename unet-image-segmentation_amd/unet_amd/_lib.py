@@ -84,6 +84,9 @@ SIGNATURES = {
     "unet_pointwise_bwd_data_bnrelu_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_data_bnrelu_wgrad": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, P, P, P, c_size_t,
                                                      P]),
+    "unet_image_block_bwd_wgrad_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "unet_image_block_bwd_wgrad": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P,
+                                           c_size_t, P]),
     "unet_conv_transpose2x2_fwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P]),
     "unet_conv_transpose2x2_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_conv_transpose2x2_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),

@@ -176,6 +176,10 @@ class UNetEngine:
         # image block (4 padded channels): data and pointwise weight gradient in one streaming pass over
         # (da, z, y) that forms dz on the fly, so dz (M x 64) is neither stored nor re-read
         self.img_fused_wgrad = True
+        # ... and, with no data gradient to produce (the network's input), its depthwise kernel
+        # gradient in the same pass: dy is contracted with x's 3x3 neighbourhood as it is formed,
+        # never stored (unet_image_block_bwd_wgrad; one launch + reductions instead of four)
+        self.img_fused_dwf = os.environ.get("UNET_IMG_DWF", "1") != "0"
         # weight gradients of the HBM-bound 64 -> 64 blocks in one pass that recomputes the
         # depthwise output y from the block's input view (unet_sepconv_bwd_filter), so their
         # forward never stores y
@@ -546,7 +550,7 @@ class UNetEngine:
         else:
             dgamma, dbeta = None, self.gvars[f"{b.name}_sepconv/bias"]
         dk, pk = self._wts(b, refresh=False)
-        img_wg = False
+        img_wg = img_all = False
         fused_bwd = self._fused_bwd(b, bb, drop_rate)
         if bb.da_rank1 and not fused_bwd:
             raise RuntimeError(f"{b.name}: rank-one da without the fused block backward")
@@ -562,7 +566,14 @@ class UNetEngine:
             bb.bn_slabs = 0
             self._flush_side()
             img_wg = self.img_fused_wgrad and drop_rate == 0.0 and b.cin == 4 and b.cout in (32, 64)
-            if img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
+            img_all = (img_wg and self.img_fused_dwf and dx0 is None and view_f.mode == L.VIEW_PLAIN
+                       and view_f.c0 == 4)
+            if img_all:  # image block: both weight gradients in one pass, neither dz nor dy stored
+                ops.image_block_bwd_wgrad(view_f.src0, n, h, w, b.wcin or b.cin, b.cout, pk, bb.scale, bb.shift,
+                                          bb.coef, bb.da, bb.z, bb.y,
+                                          self.gvars[f"{b.name}_sepconv/depthwise_kernel"],
+                                          self.gvars[f"{b.name}_sepconv/pointwise_kernel"])
+            elif img_wg:  # 4-channel image block: data + weight gradient in one pass, dz never stored
                 ops.pointwise_bwd_data_bnrelu_wgrad(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                                     bb.y, dy, self._gwts(b)[1])
             elif fused_bwd:  # dy and both weight gradients in one pass over (da, z, the input view)
@@ -584,7 +595,7 @@ class UNetEngine:
         gdk, gpk = self._gwts(b)
 
         def weight_grads():
-            if fused_bwd:  # (done by the fused pass)
+            if fused_bwd or img_all:  # (done by the fused pass)
                 return
             if bb.y_recompute:  # both kernels' gradients in one pass, y recomputed from view_in
                 ops.sepconv_bwd_filter(view_f, n, h, w, dk, dy, dz, b.cout, gdk, gpk)

@@ -543,6 +543,28 @@ def pointwise_bwd_data_bnrelu_wgrad(da: Tensor, z: Tensor, m: int, cin: int, cou
           _ptr(dpk), ws, wsb, _stream())
 
 
+def image_block_bwd_wgrad(x: Tensor, n: int, h: int, w: int, wcin: int, cout: int, pk: Tensor, scale: Tensor,
+                          shift: Tensor, coef: Tensor, da: Tensor, z: Tensor, y: Tensor, ddk: Tensor, dpk: Tensor):
+    """Both weight gradients of the image block in one pass (unet_image_block_bwd_wgrad): x the
+    (n, h, w, 4) zero-padded input, pk the padded (4, cout) kernel; ddk (3, 3, wcin, 1) and
+    dpk (1, 1, wcin, cout) are written in the Keras shapes."""
+    m = n * h * w
+    _check(x, "x", m * 4)
+    _check(da, "da", m * cout)
+    _check(z, "z", m * cout)
+    _check(y, "y", m * 4)
+    _check(pk, "pointwise_kernel", 4 * cout)
+    _check(coef, "coef", 3 * cout)
+    _check(ddk, "d_depthwise_kernel", 9 * wcin)
+    _check(dpk, "d_pointwise_kernel", wcin * cout)
+    ws, wsb = _ws(L.query("unet_image_block_bwd_wgrad_workspace", n, h, w, cout), da.device)
+    _call("unet_image_block_bwd_wgrad",
+          (2.0 * m * 4 * cout + 2.0 * m * 4 * cout + 2.0 * m * 9 * 4,
+           4.0 * (2 * m * cout + 2 * m * 4 + 4 * cout)),
+          _ptr(x), n, h, w, wcin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), _ptr(da), _ptr(z), _ptr(y),
+          _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
+
+
 # ------------------------------------------------------------ Conv2DTranspose ---
 def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor], out: Tensor):
     _check(k, "kernel", 4 * cout * x.c0)
