@@ -1287,12 +1287,18 @@ __global__ __launch_bounds__(256) void img_pw_bwd_kernel(const float* __restrict
 // Last level of the image block's weight gradients: T rows of the [4][C] | [9][4] slab summed in
 // order (double) and written in the Keras shapes of the 3-channel (wcin) input -- pointwise
 // (1, 1, wcin, C), depthwise (3, 3, wcin, 1) -- so no strided copy follows.
-__global__ __launch_bounds__(256) void img_wgrad_final_kernel(const float* __restrict__ mid, int T, int C, int wcin,
+__global__ __launch_bounds__(320) void img_wgrad_final_kernel(const float* __restrict__ mid, int T, int C, int wcin,
                                                               float* __restrict__ dpk, float* __restrict__ ddk) {
     const int SW = 4 * C + 36;
-    for (int l = threadIdx.x; l < SW; l += 256) {
+    for (int l = threadIdx.x; l < SW; l += blockDim.x) {
+        constexpr int TM = 32;  // T <= 32 (2048 slabs / 64): every row's load in flight at once
+        float v[TM];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) v[t] = mid[(int64_t)(t < T ? t : T - 1) * SW + l];
         double a = 0.0;
-        for (int t = 0; t < T; ++t) a += (double)mid[(int64_t)t * SW + l];
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+            if (t < T) a += (double)v[t];
         if (l < 4 * C) {
             const int ci = l / C, co = l - ci * C;
             if (ci < wcin) dpk[ci * C + co] = (float)a;
@@ -1715,9 +1721,10 @@ extern "C" int unet_image_block_bwd_wgrad(const float* x, int n, int h, int w, i
     UNET_CHECK_LAUNCH("unet_image_block_bwd_wgrad");
     const int64_t L = (int64_t)4 * cout + 36, sp = cdiv(S, 64) * 64, T = sp / 64;
     float* mid = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)sp * L * sizeof(float), 256));
+    UNET_CHECK_ARG(T <= 32, "unet_image_block_bwd_wgrad: %d slab rows > 32", (int)T);
     int rc = reduce_slabs(part, 64, T * L, mid, T * L, T * L, st);
     if (rc) return rc;
-    img_wgrad_final_kernel<<<1, 256, 0, st>>>(mid, (int)T, cout, wcin, d_pw_kernel, d_dw_kernel);
+    img_wgrad_final_kernel<<<1, 320, 0, st>>>(mid, (int)T, cout, wcin, d_pw_kernel, d_dw_kernel);
     UNET_CHECK_LAUNCH("unet_image_block_bwd_wgrad(final)");
     return 0;
 }
