@@ -182,5 +182,9 @@ __device__ __forceinline__ Moments moments_combine(Moments a, Moments b) {
 // floats (row == L, ld_out == L for a flat copy).  part is scratch: long, narrow reductions
 // sum chunks of slabs in place first (two fixed-order levels).
 int reduce_slabs(float* part, int S, int64_t L, float* out, int64_t row, int64_t ld_out, hipStream_t stream);
+// Two independent flat reductions over the same S slabs (one weight-gradient pass's two
+// partial arrays: pointwise + depthwise kernel, head kernel + bias) in ONE launch; outputs flat.
+int reduce_slabs_pair(const float* part_a, int64_t la, float* out_a, const float* part_b, int64_t lb, float* out_b,
+                      int S, hipStream_t stream);
 
 }  // namespace unet

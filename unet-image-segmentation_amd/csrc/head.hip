@@ -1274,9 +1274,7 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
 #undef UNET_HB1S
 #undef UNET_HB1D
         UNET_CHECK_LAUNCH("unet_head_bwd");
-        int rc = reduce_slabs(part_w, grid, x->c0, dkernel, x->c0, x->c0, st);
-        if (rc) return rc;
-        return reduce_slabs(part_b, grid, 1, dbias, 1, 1, st);
+        return reduce_slabs_pair(part_w, x->c0, dkernel, part_b, 1, dbias, grid, st);
     }
     if (head_bwdmf_ok(x, ncls)) {
         const int grid = head_bwdmf_grid(M);
@@ -1307,9 +1305,7 @@ int head_bwd_impl(const unet_view* x, int n, int h, int w, int ncls, const float
 #undef UNET_HMF
         UNET_CHECK_LAUNCH("unet_head_bwd");
         const int64_t L = (int64_t)x->c0 * ncls;
-        int rc = reduce_slabs(part_w, grid, L, dkernel, L, L, st);
-        if (rc) return rc;
-        return reduce_slabs(part_b, grid, ncls, dbias, ncls, ncls, st);
+        return reduce_slabs_pair(part_w, L, dkernel, part_b, ncls, dbias, grid, st);
     }
     float* dlg = static_cast<float*>(ws);
     const size_t dl = align_up((size_t)M * ncls * sizeof(float), 256);

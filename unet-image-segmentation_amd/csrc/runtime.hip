@@ -154,7 +154,104 @@ __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restr
         store_out(out, l, row, ld_out, t);
     }
 }
+// reduce_slabs_pair: blocks [0, a.nblk) reduce array a, the rest array b (block-uniform), each
+// thread 4 consecutive outputs over slabs g, g + 32, ... in increasing order (4 loads in flight;
+// float4 when the array is 16-B aligned with L % 4 == 0, guarded scalars otherwise), then the
+// fixed-order tree of reduce_grp4_kernel<32> -- for a float4 array the same sums, bit for bit.
+struct SlabArr {
+    const float* part;
+    int64_t L;
+    float* out;
+    int nblk;
+    int vec;
+};
+__global__ __launch_bounds__(512) void reduce_pair_kernel(SlabArr a, SlabArr b, int S) {
+    constexpr int G = 32, LQ = 512 / G;
+    const bool second = (int)blockIdx.x >= a.nblk;
+    const float* part = second ? b.part : a.part;
+    const int64_t L = second ? b.L : a.L;
+    float* out = second ? b.out : a.out;
+    const int vec = second ? b.vec : a.vec;
+    const int bx = second ? (int)blockIdx.x - a.nblk : (int)blockIdx.x;
+    const int q = threadIdx.x % LQ, g = threadIdx.x / LQ;
+    const int64_t l = ((int64_t)bx * LQ + q) * 4;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (l < L) {
+        int s = g;
+        if (vec) {
+            for (; s + 3 * G < S; s += 4 * G) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = ld4(part + (int64_t)(s + u * G) * L + l);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc[0] += (double)v[u].x; acc[1] += (double)v[u].y; acc[2] += (double)v[u].z; acc[3] += (double)v[u].w;
+                }
+            }
+            for (; s < S; s += G) {
+                const float4 v0 = ld4(part + (int64_t)s * L + l);
+                acc[0] += (double)v0.x; acc[1] += (double)v0.y; acc[2] += (double)v0.z; acc[3] += (double)v0.w;
+            }
+        } else {
+            const int nk = L - l < 4 ? (int)(L - l) : 4;
+            for (; s + 3 * G < S; s += 4 * G) {  // 4 slabs' loads in flight
+                float v[4][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {  // clamped, unconditional loads
+                        const float x = part[(int64_t)(s + u * G) * L + l + (k < nk ? k : nk - 1)];
+                        v[u][k] = k < nk ? x : 0.f;
+                    }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[k] += (double)v[u][k];
+            }
+            for (; s < S; s += G) {
+                const float* p = part + (int64_t)s * L + l;
+                float v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float x = p[k < nk ? k : nk - 1];
+                    v[k] = k < nk ? x : 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] += (double)v[k];
+            }
+        }
+    }
+    __shared__ double red[4][512];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int half = G / 2; half > 0; half >>= 1) {
+        if (g < half) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + half * LQ];
+        }
+        __syncthreads();
+    }
+    if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (l + k < L) out[l + k] = (float)red[k][q];
+    }
+}
 }  // namespace
+
+int reduce_slabs_pair(const float* part_a, int64_t la, float* out_a, const float* part_b, int64_t lb, float* out_b,
+                      int S, hipStream_t stream) {
+    UNET_CHECK_ARG(S >= 1 && la >= 1 && lb >= 1 && part_a && part_b && out_a && out_b, "reduce_slabs_pair: bad args");
+    constexpr int LQ = 16;  // output quads per block (512 threads / 32 slab groups)
+    SlabArr a{part_a, la, out_a, (int)cdiv(cdiv(la, 4), LQ),
+              la % 4 == 0 && (reinterpret_cast<uintptr_t>(part_a) & 15) == 0};
+    SlabArr b{part_b, lb, out_b, (int)cdiv(cdiv(lb, 4), LQ),
+              lb % 4 == 0 && (reinterpret_cast<uintptr_t>(part_b) & 15) == 0};
+    reduce_pair_kernel<<<(unsigned)(a.nblk + b.nblk), 512, 0, stream>>>(a, b, S);
+    UNET_CHECK_LAUNCH("reduce_slabs_pair");
+    return 0;
+}
 
 void set_error(const char* fmt, ...) {
     va_list ap;

@@ -562,9 +562,7 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
     }
     UNET_CHECK_LAUNCH(op);
     const int64_t lp = (int64_t)cin * cout, ld = (int64_t)9 * cin;
-    int rc = reduce_slabs(a.pw_slab, p.S, lp, d_pw_kernel, lp, lp, st);
-    if (rc) return rc;
-    return reduce_slabs(a.dw_slab, p.S, ld, d_dw_kernel, ld, ld, st);
+    return reduce_slabs_pair(a.pw_slab, lp, d_pw_kernel, a.dw_slab, ld, d_dw_kernel, p.S, st);
 }
 }  // namespace
 
