@@ -31,8 +31,10 @@ def _kernel_resources():
     out = {}
     with tempfile.TemporaryDirectory() as d:
         fat = os.path.join(d, "fat.bin")
-        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", str(LIB)], check=True,
-                       capture_output=True)
+        # (an explicit output file: without one objcopy rewrites the library in place, which
+        # changes its sha256 -- the key the committed PMC traffic summaries are pinned to)
+        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", str(LIB), os.path.join(d, "lib.so")],
+                       check=True, capture_output=True)
         blob = open(fat, "rb").read()
         pos, k = 0, 0
         while (i := blob.find(BUNDLE_MAGIC, pos)) >= 0:
