@@ -369,6 +369,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(res[0].item())
+    # the MeanIoU of the timed steps (warm-up + K), read before the roofline / all-reduce probe
+    # passes below train further, so 1-GPU and N-GPU lines report the same quantity
+    miou = model.mean_iou.result()
 
     # roofline pass: the same K steps again (same streams, same overlap) with the dominant
     # kernel's launches bracketed by HIP events on the stream each is issued on
@@ -440,7 +443,7 @@ def main():
         if dp_info is not None:
             out["data_parallel"] = dp_info
         if model.mean_iou is not None:
-            out["mean_io_u"] = round(model.mean_iou.result(), 6)
+            out["mean_io_u"] = round(miou, 6)
         if not args.no_roofline and world == 1 and args.encoder_batch > 0:
             del model
             torch.cuda.empty_cache()

@@ -411,7 +411,9 @@ int unet_head_bwd(const unet_view* x, int n, int h, int w, int ncls,
                   float* dbias,
                   void* ws, size_t ws_bytes, unet_stream_t stream);
 /* Head on a BNRELU view (binary; or multi-class with <= 24 classes and
- * Cin <= 64, one fused pass): unet_head_bwd plus the BatchNorm-backward
+ * Cin in {4, 8, 16, 32, 64}, one fused pass; other multi-class shapes: the
+ * _slabs query returns 0 and the call is refused -- use unet_head_bwd plus
+ * unet_bn_relu_bwd_stats): unet_head_bwd plus the BatchNorm-backward
  * partial sums of the head input's block (dx is all of its da; bn_partials
  * layout and finish as unet_dwconv3x3_bwd_data_bnstats).  _slabs: S, or 0.
  * Binary only: dx may be NULL when dlogit (m floats) is given: dx = dlogit

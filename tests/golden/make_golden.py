@@ -191,13 +191,39 @@ def train128_fixture():
 
 
 SUB = 16384  # gradient elements kept per tensor in the training-geometry fixtures
+SUB_STRIDE = 1000003  # prime: coprime to every gradient size (2^a * 3^b * 7^c, all < 2^22)
 
 
 def sub_index(size):
-    """Deterministic strided subsample of a flat tensor (all of it when it is small)."""
+    """Deterministic subsample of a flat tensor (all of it when it is small): i * P mod size for
+    i < SUB with P prime, sorted.  P is odd, so i -> i * P is a bijection mod every power of two:
+    the SUB consecutive i hit every residue of the flat index mod 2^k equally often for
+    2^k <= SUB, i.e. every output channel (the innermost Keras axis, <= 1024) of a pointwise /
+    Conv2DTranspose kernel gets SUB / Cout samples, spread over the input-channel axis too.
+    (Rounds 3-4 used the stride size // SUB, which for a 512 x 1024 kernel sampled only output
+    channels 0, 32, ..., 992 -- lane 0 of every 32-column MFMA tile)"""
     if size <= SUB:
         return np.arange(size)
-    return (np.arange(SUB, dtype=np.int64) * size) // SUB
+    assert np.gcd(size, SUB_STRIDE) == 1, size
+    return np.sort((np.arange(SUB, dtype=np.int64) * SUB_STRIDE) % size)
+
+
+def channel_norms(v):
+    """Per-output-channel and per-input-channel L2 norms of a Keras-layout gradient: the last axis
+    (pointwise / head: Cout; depthwise: the multiplier 1; Conv2DTranspose: Cin) and the second to
+    last (pointwise: Cin; depthwise: C; Conv2DTranspose: its filters f).  Vectors: |v| itself."""
+    v = np.asarray(v, np.float64)
+    if v.ndim < 2:
+        a = np.abs(v).reshape(-1)
+        return a, a
+    last = np.sqrt((v.reshape(-1, v.shape[-1]) ** 2).sum(0))
+    sec = np.sqrt((np.moveaxis(v, -2, -1).reshape(-1, v.shape[-2]) ** 2).sum(0))
+    return last, sec
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
 def class_masks(n, h, w, ncls, seed):
@@ -233,6 +259,7 @@ def train_big_fixture(size, n, ncls, x_seed, w_seed):
         out["gnorm:" + k] = np.linalg.norm(flat)
         out["g128:" + k] = flat[:128]
         out["gsub:" + k] = flat[sub_index(flat.size)].astype(np.float32)
+        out["cn_last:" + k], out["cn_sec:" + k] = channel_norms(v)
     for k, v in w.items():
         if k in g:
             p1, _, _ = K.adamw_update(v, g[k], np.zeros_like(v), np.zeros_like(v), 1, 2e-3, 1e-4)
@@ -250,6 +277,9 @@ def train_big_fixture(size, n, ncls, x_seed, w_seed):
         out["e32:" + k] = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
         i = sub_index(b.size)
         out["e32sub:" + k] = np.linalg.norm(a[i] - b[i]) / max(np.linalg.norm(b[i]), 1e-30)
+        l32, s32 = channel_norms(g32[k])
+        out["e32cn_last:" + k] = rel_l2(l32, out["cn_last:" + k])
+        out["e32cn_sec:" + k] = rel_l2(s32, out["cn_sec:" + k])
     return out
 
 

@@ -81,6 +81,34 @@ def test_training_geometry_goldens_consistent(name):
         p1, _, _ = K.adamw_update(w0, g["g128:" + k][:n], np.zeros(n), np.zeros(n), 1, 2e-3, 1e-4)
         assert np.allclose(p1, g["new256:" + k][:n], rtol=1e-12, atol=1e-15), k
         assert 0.0 <= float(g["e32sub:" + k]) < 0.1 and 0.0 <= float(g["e32:" + k]) < 0.1, k
+        # per-channel norms: one per channel of each axis, and each axis's norms square-sum to
+        # the tensor norm
+        shape = next(s.shape for s in specs if s.name == k)
+        last, sec = g["cn_last:" + k], g["cn_sec:" + k]
+        if len(shape) >= 2:
+            assert last.shape == (shape[-1],) and sec.shape == (shape[-2],), k
+        for v in (last, sec):
+            assert abs(np.linalg.norm(v) - float(g["gnorm:" + k])) <= 1e-9 * float(g["gnorm:" + k]) + 1e-30, k
+        assert 0.0 <= float(g["e32cn_last:" + k]) < 0.1 and 0.0 <= float(g["e32cn_sec:" + k]) < 0.1, k
+
+
+def test_gradient_subsample_hits_every_channel():
+    """the training-geometry subsample covers every output channel and every
+    input channel of each large pointwise / Conv2DTranspose kernel (so every MFMA lane / column of
+    a tile is checked), not only the channels that are multiples of the old stride."""
+    from unet_amd.params import unet_variables
+    for ncls in (1, 21):
+        for s in unet_variables(3, ncls, True, MG.FULL):
+            n = int(np.prod(s.shape))
+            i = MG.sub_index(n)
+            assert np.unique(i).size == i.size == min(n, MG.SUB)
+            if len(s.shape) >= 2 and s.shape[-1] > 1:
+                assert np.unique(i % s.shape[-1]).size == s.shape[-1], s.name
+                assert np.unique((i // s.shape[-1]) % s.shape[-2]).size == s.shape[-2], s.name
+                # every residue mod 32 of both channel axes
+                for ax, c in ((i % s.shape[-1], s.shape[-1]), ((i // s.shape[-1]) % s.shape[-2], s.shape[-2])):
+                    if c >= 32:
+                        assert np.bincount(ax % 32, minlength=32).min() > 0, s.name
 
 
 @pytest.mark.gpu

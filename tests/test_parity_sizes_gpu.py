@@ -241,8 +241,8 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
         sd = np.sqrt(var + BN_EPS)
         e = max(float(np.abs(dmu - mu).max(initial=0) / sd.max()), float((np.abs(dvar - var) / (var + BN_EPS)).max()))
         bn_worst = max(bn_worst, e)
-    # gradients on the committed subsample
-    errs, bad = {}, {}
+    # gradients on the committed subsample (every residue of both channel axes, MG.sub_index)
+    errs, bad, cn_errs, cn_bad = {}, {}, {}, {}
     for k, v in grads.items():
         flat = v.reshape(-1).astype(np.float64)
         ref = g["gsub:" + k].astype(np.float64)
@@ -252,6 +252,14 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
         lim = max(2e-3, float(g["e32sub:" + k]))  # (2 e32 through round 3; worst ratio seen 0.53)
         if e > lim:
             bad[k] = (e, lim)
+        # per-output-channel / per-input-channel norms of the WHOLE tensor (every column, not a
+        # sample), against max(2e-3, e32) with e32 the float32 oracle's full-tensor distance
+        last, sec = MG.channel_norms(v)
+        el, es = MG.rel_l2(last, g["cn_last:" + k]), MG.rel_l2(sec, g["cn_sec:" + k])
+        cn_errs[k] = (el, es, float(g["e32cn_last:" + k]), float(g["e32cn_sec:" + k]))
+        lim_cn = max(2e-3, float(g["e32:" + k]))
+        if max(el, es) > lim_cn:
+            cn_bad[k] = (el, es, lim_cn)
     worst = sorted(errs.items(), key=lambda r: -r[1])[:5]
     # each tensor's error against the float32 oracle's own distance to float64 on the same subsample
     ratios = {k: errs[k] / max(float(g["e32sub:" + k]), 1e-30) for k in errs}
@@ -261,14 +269,17 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
         bb = A.blocks[b.name]
         pre = bb.z.double() * bb.scale.double() + bb.shift.double()
         near0 += int((pre.abs() < 1e-6 * (bb.shift.double().abs().max() + 1)).sum())
+    worst_cn = sorted(((k, *v) for k, v in cn_errs.items()), key=lambda r: -max(r[1], r[2]))[:5]
     _log({"test": fixture, "x3": x3, "recompute128": recompute128, "worst_ratio_to_e32sub": worst_ratio,
           "loss": float(res[0]), "loss_ref": float(g["loss"]), "dice": float(res[1]),
           "bn_stats_worst_rel": bn_worst, "max_grad_rel_l2_sub": worst[0][1], "worst_grads": worst,
+          "worst_channel_norms(name, last, second, e32 last, e32 second)": worst_cn,
           "max_fp32_oracle_rel_l2": max(float(g["e32:" + k]) for k in grads), "relu_near_ties": near0})
     assert abs(res[0] - g["loss"]) < 1e-5 and abs(res[1] - g["dice"]) < 1e-5
     assert bn_worst < 1e-4, bn_worst
     assert set(k[6:] for k in g if k.startswith("gnorm:")) == set(grads)
     assert not bad, bad
+    assert not cn_bad, cn_bad
     for k, v in g.items():
         if k.startswith("gnorm:"):
             hn = float(np.linalg.norm(grads[k[6:]]))
@@ -327,6 +338,16 @@ def test_split_precision_relu_decisions_train256c21():
     gd = {k: float(np.linalg.norm(runs[1][1][k] - runs[0][1][k]) / max(np.linalg.norm(runs[0][1][k]), 1e-30))
           for k in runs[0][1]}
     worst = sorted(gd.items(), key=lambda r: -r[1])[:5]
+    # the same distances on the metric the training-geometry test gates on: the committed
+    # subsample, each device run against the float64 oracle there and against each other
+    sub = {}
+    for k in runs[0][1]:
+        i = MG.sub_index(runs[0][1][k].size)
+        ref = g["gsub:" + k].astype(np.float64)
+        a, b = runs[0][1][k].reshape(-1)[i], runs[1][1][k].reshape(-1)[i]
+        sub[k] = (MG.rel_l2(b, a), MG.rel_l2(a, ref), MG.rel_l2(b, ref), float(g["e32sub:" + k]))
+    worst_sub = sorted(((k, *v) for k, v in sub.items()), key=lambda r: -r[1])[:5]
     _log({"test": "x3_vs_fp32_relu_decisions[train256c21]", "relu_flips_per_block": flips,
-          "flips_total": sum(flips.values()), "elements": total, "grad_rel_l2_x3_vs_fp32_worst": worst})
+          "flips_total": sum(flips.values()), "elements": total, "grad_rel_l2_x3_vs_fp32_worst": worst,
+          "sub(name, x3 vs fp32, fp32 vs oracle, x3 vs oracle, e32sub)": worst_sub})
     assert sum(flips.values()) <= 1e-5 * total, flips

@@ -36,9 +36,59 @@ template <class F> static double timeit(F f, int it = 20) {
     return ms * 1e3 / it;
 }
 
+#include "gemm_v2.inc"
+#include "gemm_wv2.inc"
 #include "gemm_lab_variants.inc"
 
+template <int BP, int BQ, int BK, bool V2>
+static void wlaunch(const WgradArgs& a, const WgradPlan& w) {
+    dim3 grid((unsigned)w.tiles, (unsigned)w.S);
+    if (V2) gemm_wgrad_v2<BP, BQ, BK, W_PLAIN, false, W_PLAIN, false><<<grid, 256>>>(a);
+    else gemm_wgrad_vec<BP, BQ, W_PLAIN, false, W_PLAIN, false><<<grid, 256>>>(a);
+}
+template <int BP, int BQ>
+static void wgrad_variants(WgradArgs a, const WgradPlan& w, float* s0, float* s1, double fl, size_t n) {
+    a.slab = s0; wlaunch<BP, BQ, 16, false>(a, w); CK(hipDeviceSynchronize());
+    auto V = [&](const char* name, auto fn) {
+        CK(hipMemset(s1, 0, n * 4));
+        double us = timeit([&] { fn(); });
+        double d = maxdiff(s1, s0, n);
+        printf("  %-34s %8.1f us %7.1f TF/s  diff %.2e\n", name, us, fl / us * 1e-6, d);
+    };
+    a.slab = s1;
+    V("product wgrad_vec", [&] { wlaunch<BP, BQ, 16, false>(a, w); });
+    V("v2 BK16", [&] { wlaunch<BP, BQ, 16, true>(a, w); });
+    V("v2 BK32", [&] { wlaunch<BP, BQ, 32, true>(a, w); });
+}
+static void run_wgrad_lab() {
+    struct WS { int64_t M; int P, Q; };
+    std::vector<WS> ws = {{1048576, 64, 64}, {262144, 64, 128}, {262144, 128, 128}, {65536, 128, 256}, {65536, 256, 256},
+                          {16384, 256, 512}, {16384, 512, 512}, {4096, 512, 1024}, {4096, 1024, 1024},
+                          {16384, 1024, 512}, {65536, 512, 256}, {262144, 256, 128}, {1048576, 128, 64}};
+    for (auto& s : ws) {
+        float* A = dalloc(s.M * s.P, 1.f, 11);
+        float* B = dalloc(s.M * s.Q, 1.f, 12);
+        WgradArgs a{};
+        unet_view va{}; va.mode = UNET_VIEW_PLAIN; va.c0 = s.P; va.src0 = A;
+        unet_view vb{}; vb.mode = UNET_VIEW_PLAIN; vb.c0 = s.Q; vb.src0 = B;
+        a.a = make_dview(va); a.b = make_dview(vb); a.P = s.P; a.Q = s.Q; a.M = s.M;
+        WgradPlan w = wgrad_plan(s.M, s.P, s.Q);
+        a.mslice = w.mslice;
+        const size_t n = (size_t)w.S * s.P * s.Q;
+        float *s0, *s1; CK(hipMalloc(&s0, n * 4)); CK(hipMalloc(&s1, n * 4));
+        const double fl = 2.0 * s.M * s.P * s.Q;
+        printf("WGRAD M=%ld P=%d Q=%d tiles %d S %d mslice %ld\n", (long)s.M, s.P, s.Q, w.tiles, w.S, (long)w.mslice);
+        if (w.bp == 128 && w.bq == 128) wgrad_variants<128, 128>(a, w, s0, s1, fl, n);
+        else if (w.bp == 128) wgrad_variants<128, 64>(a, w, s0, s1, fl, n);
+        else if (w.bq == 128) wgrad_variants<64, 128>(a, w, s0, s1, fl, n);
+        else wgrad_variants<64, 64>(a, w, s0, s1, fl, n);
+        CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(s0)); CK(hipFree(s1));
+        fflush(stdout);
+    }
+}
+
 int main(int argc, char** argv) {
+    if (getenv("LAB_WGRAD")) { run_wgrad_lab(); return 0; }
     struct Shape { int64_t M; int K, N; int mode; };  // mode 0: fwd (B [K][N]), 1: dgrad BN-bwd (B [N][K])
     std::vector<Shape> shapes = {
         {1048576, 64, 64, 0}, {262144, 128, 128, 0}, {65536, 256, 256, 0}, {16384, 512, 512, 0}, {4096, 1024, 1024, 0},

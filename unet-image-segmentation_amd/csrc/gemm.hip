@@ -1711,6 +1711,9 @@ extern "C" int unet_image_block_bwd_wgrad(const float* x, int n, int h, int w, i
     UNET_CHECK_ARG(ws && ws_bytes >= need, "unet_image_block_bwd_wgrad: workspace %zu < %zu", ws_bytes, need);
     hipStream_t st = as_stream(stream);
     const int S = img_pw_slabs(m, cout);
+    const int64_t L = (int64_t)4 * cout + 36, sp = cdiv(S, 64) * 64, T = sp / 64;
+    // checked before any launch (img_wgrad_final_kernel holds <= 32 slab rows in registers)
+    UNET_CHECK_ARG(T <= 32, "unet_image_block_bwd_wgrad: %d slab rows > 32", (int)T);
     float* part = static_cast<float*>(ws);
     if (cout == 64)
         img_pw_bwd_kernel<16, true><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, nullptr, part, x,
@@ -1719,9 +1722,7 @@ extern "C" int unet_image_block_bwd_wgrad(const float* x, int n, int h, int w, i
         img_pw_bwd_kernel<8, true><<<S, 256, 0, st>>>(da, z, m, pw_kernel, scale, shift, coef, y, nullptr, part, x,
                                                       h, w);
     UNET_CHECK_LAUNCH("unet_image_block_bwd_wgrad");
-    const int64_t L = (int64_t)4 * cout + 36, sp = cdiv(S, 64) * 64, T = sp / 64;
     float* mid = reinterpret_cast<float*>(static_cast<char*>(ws) + align_up((size_t)sp * L * sizeof(float), 256));
-    UNET_CHECK_ARG(T <= 32, "unet_image_block_bwd_wgrad: %d slab rows > 32", (int)T);
     int rc = reduce_slabs(part, 64, T * L, mid, T * L, T * L, st);
     if (rc) return rc;
     img_wgrad_final_kernel<<<1, 320, 0, st>>>(mid, (int)T, cout, wcin, d_pw_kernel, d_dw_kernel);

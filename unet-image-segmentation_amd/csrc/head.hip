@@ -1202,7 +1202,7 @@ extern "C" int unet_head_bwd_bnstats(const unet_view* x, int n, int h, int w, in
                                      unet_stream_t stream) {
     UNET_CHECK_ARG(unet_head_bwd_bnstats_slabs(x, n, h, w, ncls) > 0,
                    "unet_head_bwd_bnstats: needs a BNRELU view with Cin %% 4 == 0 (multi-class: <= 24 classes, "
-                   "Cin <= 64)");
+                   "Cin in {4, 8, 16, 32, 64})");
     UNET_CHECK_ARG(ncls == 1 || dlogit == nullptr, "unet_head_bwd_bnstats: the dlogit form is binary-only");
     UNET_CHECK_ARG(bn_partials, "unet_head_bwd_bnstats: null bn_partials");
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_head_bwd_bnstats: mean and rstd go together");

@@ -80,10 +80,13 @@ def load_image(path, size, mode):
 
 class PairLoader:
     """cache_bytes: decoded, resized samples are kept as uint8 (256 x 256 x 4 B = 256 KiB per
-    pair at 256 x 256) up to this budget (default 8 GiB divided among this host's data-parallel
-    ranks, so a train + val loader pair on every rank of a node holds at most 16 GiB), so PNG decoding (~25 ms per 960 x 540 frame on one
-    core, tools/bench_loader.py) is paid once per file, not once per epoch: the decode and resize
-    are deterministic, so the batches are identical to decoding every epoch."""
+    pair at 256 x 256) up to this budget, so PNG decoding (~25 ms per 960 x 540 frame on one core,
+    tools/bench_loader.py) is paid once per file, not once per epoch: the decode and resize are
+    deterministic, so the batches are identical to decoding every epoch.  Default: 16 GiB per
+    loader (about 64k pairs at 256 x 256, whatever the rank count); a host-wide budget for all of
+    a node's loaders can be set with UNET_LOADER_CACHE_HOST_GB (divided among the node's ranks and
+    their train + val loaders).  No loader throughput was measured at 8 ranks, so the default does
+    not shrink with the rank count."""
 
     def __init__(self, frames_dir, masks_dir, size, batch_size, seed, shuffle=True, horizontal_flip=False, rank=0,
                  world=1, workers=16, cache_bytes=None):
@@ -98,8 +101,12 @@ class PairLoader:
         self.samples = len(self.frames)
         self.workers = max(1, int(workers))
         self._pool = None
-        if cache_bytes is None:  # host-wide: 8 GiB per loader (train + val) shared by this node's ranks
-            cache_bytes = (8 << 30) // local_world_size()
+        if cache_bytes is None:
+            host_gb = os.environ.get("UNET_LOADER_CACHE_HOST_GB")
+            if host_gb:  # one host-wide budget over this node's ranks x (train + val) loaders
+                cache_bytes = int(float(host_gb) * (1 << 30)) // (2 * local_world_size())
+            else:
+                cache_bytes = 16 << 30
         self.cache_bytes = int(cache_bytes)
         self._cache = {}
         self._cached_bytes = 0
