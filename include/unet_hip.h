@@ -362,14 +362,17 @@ int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w,
                                const float* dout, float* dx, float* dkernel,
                                float* dbias, void* ws, size_t ws_bytes,
                                unet_stream_t stream);
-/* Data gradient only, for a BNRELU view without dropout (the decoder block2 /
- * bottleneck output feeding the upsample, u_net.py:88): dx is then the whole da
- * of the view's block, so the GEMM epilogue also emits that block's
- * BatchNorm-backward partials in the unet_dwconv3x3_bwd_data_bnstats format
- * (S = _slabs(...) slabs of 128 rows; mean/rstd NULL when
- * use_batch_norm=False; finish with unet_bn_relu_bwd_stats_finish).  Replaces
- * unet_bn_relu_bwd_stats's separate pass over (da, z).  _slabs: 0 if the view
- * or shape has no such path.                                                 */
+/* Data gradient only, for a BNRELU view (the decoder block2 / bottleneck
+ * output feeding the upsample, u_net.py:88): dx is then the whole da of the
+ * view's block, so the GEMM epilogue also emits that block's BatchNorm-backward
+ * partials in the unet_dwconv3x3_bwd_data_bnstats format (S = _slabs(...)
+ * slabs of 128 rows; mean/rstd NULL when use_batch_norm=False; finish with
+ * unet_bn_relu_bwd_stats_finish).  Replaces unet_bn_relu_bwd_stats's separate
+ * pass over (da, z).  A view with dropout (the bottleneck's, u_net.py:77-78;
+ * round 5, no signature change): the partials are those of g = da * mask, as
+ * unet_bn_relu_bwd_stats(..., drop_rate, drop_seed, ...) forms them; dx stays
+ * the gradient w.r.t. the dropout output.  _slabs: 0 if the view or shape has
+ * no such path.                                                              */
 int unet_conv_transpose2x2_bwd_data_bnstats_slabs(const unet_view* x, int n,
                                                   int h, int w, int cout);
 int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h,

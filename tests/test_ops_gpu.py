@@ -679,21 +679,25 @@ def test_fused_sepconv_unsupported_shapes(ops):
 
 
 @pytest.mark.parametrize("use_bn", [True, False])
+@pytest.mark.parametrize("drop", [0.0, 0.2])
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 8, 8, 128, 64), (1, 5, 7, 64, 32), (3, 4, 6, 256, 128),
                                             (2, 16, 16, 128, 128), (4, 64, 144, 128, 64)])  # > 256 slabs
-def test_convt_bwd_data_bnstats(ops, use_bn, n, h, w, cin, cout):
+def test_convt_bwd_data_bnstats(ops, use_bn, drop, n, h, w, cin, cout):
     """Conv2DTranspose data gradient that also emits the BN-backward partials of the block below
-    (u_net.py:88 upsample fed by a BN+ReLU output): dx bitwise equal to the plain launch,
+    (u_net.py:88 upsample fed by a BN+ReLU output; with drop > 0 through the bottleneck's Dropout,
+    u_net.py:77-78, so the partials carry the mask): dx bitwise equal to the plain launch,
     statistics equal to unet_bn_relu_bwd_stats's and to float64 numpy."""
     rng = np.random.default_rng(n * 1000 + h * 10 + cin + cout)
     a, t = _view_inputs(rng, 1, n, h, w, cin)
     v = _mk_view(ops, 1, t)
+    seed = 4242
+    if drop > 0.0:
+        v = v.dropout(drop, seed)
     k = dev(f32(rng.standard_normal((2, 2, cout, cin)) * 0.1))
     dout = dev(f32(rng.standard_normal((n, 2 * h, 2 * w, cout))))
     S = ops.conv_transpose2x2_bwd_data_bnstats_slabs(v, n, h, w, cout)
     m = n * h * w
     assert S == (m + 127) // 128
-    assert ops.conv_transpose2x2_bwd_data_bnstats_slabs(v.dropout(0.2, 1), n, h, w, cout) == 0
     mean = dev(f32(rng.standard_normal(cin) * 0.1))
     rstd = dev(f32(1.0 + rng.random(cin)))
     part = torch.zeros(ops.bn_stats_partials_numel(S, cin), device="cuda")  # counters zero
@@ -710,12 +714,14 @@ def test_convt_bwd_data_bnstats(ops, use_bn, n, h, w, cin, cout):
             ops.bn_relu_bwd_stats_finish(part, S, m, cin, mean, rstd, use_bn, dg if use_bn else None, db, coef)
             assert not torch.any(part[-((cin + 63) // 64):].view(torch.int32))
         else:
-            ops.bn_relu_bwd_stats(dx_p, t["src0"], m, cin, mean, rstd, t["sc0"], t["sh0"], use_bn, 0.0, 0,
+            ops.bn_relu_bwd_stats(dx_p, t["src0"], m, cin, mean, rstd, t["sc0"], t["sh0"], use_bn, drop, seed,
                                   dg if use_bn else None, db, coef)
         outs.append((host(dg), host(db), host(coef)))
     for x, y in zip(outs[0], outs[1]):
         assert rel_err(x, y) < 2e-5
     da = host(dx_p).astype(np.float64).reshape(-1, cin)
+    if drop > 0.0:  # the documented counter-based mask (oracle/keras_ops.py dropout_mult)
+        da = da * K.dropout_mult(seed, (n, h, w, cin), drop).reshape(-1, cin)
     z = a["src0"].astype(np.float64).reshape(-1, cin)
     g = np.where(z * a["sc0"] + a["sh0"] > 0, da, 0.0)
     assert rel_err(outs[0][1], g.sum(0)) < 1e-5

@@ -58,6 +58,8 @@ struct RowsArgs {
     float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
     const float *bsc, *bsh, *bmu, *brs;  // E_BNPART: per-column BN scale/shift, mean/rstd (NULL: no xhat)
     float* bnpart;                       // E_BNPART: [cdiv(M, 128)][2][N] partial sums
+    float ep_rate, ep_inv_keep;          // E_BNPART: dropout between the block and C's consumer (rate 0: none);
+    uint64_t ep_seed;                    //   g also carries the mask of element (m, n) (common.h drop_mult)
     int ko;  // lab build only (UNET_ROWS_KO): knock-out bits for timing decompositions, else 0
 };
 #ifdef UNET_LAB_BUILD
@@ -472,9 +474,26 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
 // BK + 8 bf16 = conflict-free ds_read_b128), and every 16-deep k step runs the six
 // v_mfma_f32_32x32x16_bf16 of mfma_x6 per 32x32 tile: 6 x 32 cycles instead of the 8 x 64 of
 // v_mfma_f32_32x32x2_f32, at fp32 accuracy.  Loads, operand views and epilogues are shared.
+#ifdef UNET_LAB_BUILD
+// lab: ko bits 8-15 = stagger (that many s_sleep 32, ~2048 cycles each) for the second half of the
+// grid's blocks (bit 16: the odd blocks instead), so the two blocks sharing a CU do not run in lockstep
+__device__ __forceinline__ void lab_stagger(int ko) {
+    const int n = (ko >> 8) & 255;
+    if (n == 0) return;
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x, tot = gridDim.x * gridDim.y;
+    const bool late = (ko & 0x10000) ? (lin & 1) : (lin >= tot / 2);
+    if (late)
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
+}
+#define ROWS_STAGGER(g) lab_stagger((g).ko)
+#else
+#define ROWS_STAGGER(g) ((void)0)
+#endif
+
 template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC, bool X6 = false>
 __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     main_stream_prio();
+    ROWS_STAGGER(g);
     constexpr int LR = BK + 4;     // A (and k-contiguous B) LDS row stride, floats
     constexpr int LB = BN + 4;     // k-major B LDS row stride (n-contiguous weights)
     constexpr int XR = BK + 8;     // X6: bf16 row stride of the split planes
@@ -808,7 +827,10 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const bool in = full || rb0 + acc_row(r, 0) < M_rem;
-                        const float gm = (in && fmaf(zv[r], sc, sh) > 0.f) ? acc[tm][tn][r] : 0.f;
+                        float gm = (in && fmaf(zv[r], sc, sh) > 0.f) ? acc[tm][tn][r] : 0.f;
+                        if (g.ep_rate > 0.f)  // (uniform) the consumer read the activation through dropout
+                            gm *= drop_mult(g.ep_seed, (uint64_t)(m0 + rb0 + acc_row(r, 0)) * g.N + n, g.ep_rate,
+                                            g.ep_inv_keep);
                         s1 += gm;
                         s2 = fmaf(gm, (zv[r] - mu) * rs, s2);
                     }
@@ -1334,9 +1356,12 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     // rows) take 64-wide N tiles, twice the blocks
     const bool narrow = lab_knob("UNET_ROWS_NARROW", 1) && a.N > 64 && cdiv(a.M, 128) * cdiv(a.N, 128) < 256;
     if (amode == A_BNBWD) {
-        if (a.N <= 64 || narrow) return RowsCfg{64, 32};
+        // lab: UNET_BNBWD_BK16 = 1 stages BK = 16 (40 KB of LDS instead of 72 KB at 128 columns:
+        // co-residency with the side stream's weight-gradient blocks)
+        const int bk = lab_knob("UNET_BNBWD_BK16", 0) ? 16 : 32;
+        if (a.N <= 64 || narrow) return RowsCfg{64, bk};
         if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
-        return RowsCfg{128, 32};
+        return RowsCfg{128, bk};
     }
     const int bk32_k = lab_knob("UNET_BK32_MIN_K", 256);  // smallest K that takes BK = 32
     if (a.N <= 64) return RowsCfg{64, 16};
@@ -1856,7 +1881,8 @@ extern "C" int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int 
 }
 
 extern "C" int unet_conv_transpose2x2_bwd_data_bnstats_slabs(const unet_view* x, int n, int h, int w, int cout) {
-    if (!x || x->mode != UNET_VIEW_BNRELU || x->drop_rate != 0.f || n <= 0 || h <= 0 || w <= 0 || cout <= 0)
+    if (!x || x->mode != UNET_VIEW_BNRELU || !(x->drop_rate >= 0.f && x->drop_rate < 1.f) || n <= 0 || h <= 0 ||
+        w <= 0 || cout <= 0)
         return 0;
     if (x->c0 % 4 || cout % 4) return 0;
     const int64_t M = (int64_t)n * h * w;
@@ -1870,8 +1896,8 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n
                                                        unet_stream_t stream) {
     if (check_view(x, "unet_conv_transpose2x2_bwd_data_bnstats")) return -1;
     const int S = unet_conv_transpose2x2_bwd_data_bnstats_slabs(x, n, h, w, cout);
-    UNET_CHECK_ARG(S > 0, "unet_conv_transpose2x2_bwd_data_bnstats: needs a BNRELU view without dropout and "
-                          "channel counts divisible by 4");
+    UNET_CHECK_ARG(S > 0, "unet_conv_transpose2x2_bwd_data_bnstats: needs a BNRELU view (dropout rate in [0, 1)) "
+                          "and channel counts divisible by 4");
     UNET_CHECK_ARG(kernel && dout && dx && bn_partials && x->scale0 && x->shift0,
                    "unet_conv_transpose2x2_bwd_data_bnstats: bad args");
     UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "unet_conv_transpose2x2_bwd_data_bnstats: mean/rstd go together");
@@ -1895,6 +1921,11 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n
     a.bmu = mean;
     a.brs = rstd;
     a.bnpart = bn_partials;
+    // a dropout view (the bottleneck output, u_net.py:77-78): the partials are those of the
+    // BN + ReLU backward of g = da * mask, as unet_bn_relu_bwd_stats forms them
+    a.ep_rate = x->drop_rate;
+    a.ep_inv_keep = x->drop_rate > 0.f ? 1.0f / (1.0f - x->drop_rate) : 1.0f;
+    a.ep_seed = x->drop_seed;
     UNET_CHECK_ARG(rows_vec_ok(a, A_UNSHUFFLE) && ((uintptr_t)dx | (uintptr_t)x->src0) % 16 == 0,
                    "unet_conv_transpose2x2_bwd_data_bnstats: operands must be 16-B aligned");
     return launch_rows<A_UNSHUFFLE, false, E_BNPART>(a, as_stream(stream), "unet_conv_transpose2x2_bwd_data_bnstats");

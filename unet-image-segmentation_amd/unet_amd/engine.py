@@ -91,6 +91,7 @@ class BlockBufs:
     coef: Optional[torch.Tensor] = None  # BN-backward coefficients (mean, dbeta/M, rstd*dgamma/M)
     bnpart: Optional[torch.Tensor] = None  # BN-backward partial sums emitted by the producer of da
     bn_slabs: int = 0  # > 0: bnpart holds this many fresh slabs for the next backward of the block
+    bn_masked: bool = False  # ... and they already carry the dropout mask between the block and its consumer
     bnpart_s: int = -1  # the slab count bnpart's counters were last laid out for
     y_recompute: bool = False  # last training forward kept no y: the weight grads recompute it
     zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
@@ -556,7 +557,7 @@ class UNetEngine:
             raise RuntimeError(f"{b.name}: rank-one da without the fused block backward")
         if self.fuse_bn_bwd and b.cin % 4 == 0 and b.cout % 4 == 0:
             # BN + ReLU backward statistics, then dz formed inside the data-gradient GEMM's loads
-            if bb.bn_slabs and drop_rate == 0.0:  # partials already emitted by the producer of da
+            if bb.bn_slabs and (drop_rate == 0.0 or bb.bn_masked):  # partials emitted by the producer of da
                 ops.bn_relu_bwd_stats_finish(bb.bnpart[:ops.bn_stats_partials_numel(bb.bn_slabs, b.cout)],
                                              bb.bn_slabs, m, b.cout, bb.mean, bb.rstd, self.use_bn, dgamma, dbeta,
                                              bb.coef)
@@ -564,6 +565,7 @@ class UNetEngine:
                 ops.bn_relu_bwd_stats(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn,
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
+            bb.bn_masked = False
             self._flush_side()
             img_wg = self.img_fused_wgrad and drop_rate == 0.0 and b.cin == 4 and b.cout in (32, 64)
             img_all = (img_wg and self.img_fused_dwf and dx0 is None and view_f.mode == L.VIEW_PLAIN
@@ -700,6 +702,7 @@ class UNetEngine:
                                                        pb.mean if self.use_bn else None,
                                                        pb.rstd if self.use_bn else None, self._bnpart(pb, S, xv.c0))
                 pb.bn_slabs = S
+                pb.bn_masked = xv.drop_rate > 0.0  # (the bottleneck's dropout: the partials carry its mask)
             else:
                 ops.conv_transpose2x2_bwd(xv, n, h, w, fi, uk, A.dup[stage], pb.da, None, None)
             if self.overlap:
