@@ -4,6 +4,7 @@
 // and max |diff| against the product kernel's output.
 #include "gemm.hip"
 #include <vector>
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -104,7 +105,8 @@ int main(int argc, char** argv) {
     for (auto& s : shapes) {
         ++si;
         if (only && atoi(only) != si) continue;
-        const int64_t M = s.M; const int K = s.K, N = s.N;
+        const int lab_batch = getenv("LAB_BATCH") ? atoi(getenv("LAB_BATCH")) : 16;  // shapes are batch 16
+        const int64_t M = s.M * lab_batch / 16; const int K = s.K, N = s.N;
         if (getenv("LAB_MODE") && atoi(getenv("LAB_MODE")) != s.mode) continue;
         float* A = dalloc(M * K, 1.f, 1);
         float* Z = dalloc(M * K, 1.f, 2);
@@ -118,7 +120,7 @@ int main(int argc, char** argv) {
         unet_view v{}; v.mode = UNET_VIEW_PLAIN; v.c0 = K; v.src0 = A;
         a.a = make_dview(v);
         a.M = M; a.K = K; a.N = N; a.B = B; a.ldc = N;
-        const int hw = (int)lround(sqrt((double)(M / 16)));  // convT shapes: batch 16, square levels
+        const int hw = (int)lround(sqrt((double)(M / lab_batch)));  // convT shapes: square levels
         if (s.mode == 0) { a.sbk = N; a.sbn = 1; a.stats = stats; }
         else if (s.mode == 2) { a.sbk = 1; a.sbn = K; a.bias = sc; a.sH = hw; a.sW = hw; a.sf = N / 4; }
         else if (s.mode == 3) {  // A = dU (n, 2h, 2w, K/4) read unshuffled: M x K elements either way

@@ -60,6 +60,20 @@ __global__ __launch_bounds__(256) void mfma_k(const float* __restrict__ src, flo
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[a].w, fb[b].w, acc[a][b], 0, 0, 0);
                 }
         }
+        if constexpr (MODE >= 4) {  // + VALU work per stage (MODE 4: 64, MODE 5: 128 independent fmaf)
+            constexpr int NV = MODE == 4 ? 16 : 32;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                g4.x = fmaf(g4.x, 1.0001f, fa[0].x);
+                g4.y = fmaf(g4.y, 1.0001f, fa[0].y);
+                g4.z = fmaf(g4.z, 1.0001f, fa[1].x);
+                g4.w = fmaf(g4.w, 1.0001f, fa[1].y);
+            }
+        }
+        if constexpr (MODE >= 6) {  // + 8 ds_write_b128 per stage (the GEMM's A + B staging)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) *reinterpret_cast<float4*>(&L[buf ^ 1][(tid * 4 + r * 1024) % (128 * 36 * 2 - 4)]) = g4;
+        }
         if constexpr (MODE >= 1) __syncthreads();
     }
     float s = g4.x + g4.y + g4.z + g4.w;
@@ -114,6 +128,11 @@ int main() {
     run<1>("LDS fragments + barrier", src, out, st, blocks, iters);
     run<2>("+ streaming global read", src, out, st, blocks, iters);
     run<3>("+ LDS write of it", src, out, st, blocks, iters);
+    run<4>("+ 64 VALU fma / stage", src, out, st, blocks, iters);
+    run<5>("+ 128 VALU fma / stage", src, out, st, blocks, iters);
+    run<6>("+ 128 VALU + 8 ds_write_b128", src, out, st, blocks, iters);
+    run<3>("mode 3, 32 stages (K=512 at BK16)", src, out, st, blocks, 32);
+    run<6>("mode 6, 32 stages", src, out, st, blocks, 32);
     run<0>("registers only (again)", src, out, st, blocks, iters);
     return 0;
 }

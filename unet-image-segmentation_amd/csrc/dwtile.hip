@@ -428,11 +428,11 @@ int filter_blocks(const TilePlan& p) {
 
 #define UNET_TILE_DISPATCH_QT(KERNEL, MODE, DROP, GRID, ...)                       \
     switch (p.qt) {                                                                \
-        case 16: KERNEL<MODE, DROP, 16><<<GRID, 256, 0, st>>>(__VA_ARGS__); break; \
-        case 8: KERNEL<MODE, DROP, 8><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
-        case 4: KERNEL<MODE, DROP, 4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
-        case 2: KERNEL<MODE, DROP, 2><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;   \
-        default: KERNEL<MODE, DROP, 1><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;  \
+        case 16: KERNEL<MODE, DROP, 16><<<GRID, 256, tile_lds_pad, st>>>(__VA_ARGS__); break; \
+        case 8: KERNEL<MODE, DROP, 8><<<GRID, 256, tile_lds_pad, st>>>(__VA_ARGS__); break;   \
+        case 4: KERNEL<MODE, DROP, 4><<<GRID, 256, tile_lds_pad, st>>>(__VA_ARGS__); break;   \
+        case 2: KERNEL<MODE, DROP, 2><<<GRID, 256, tile_lds_pad, st>>>(__VA_ARGS__); break;   \
+        default: KERNEL<MODE, DROP, 1><<<GRID, 256, tile_lds_pad, st>>>(__VA_ARGS__); break;  \
     }
 #define UNET_TILE_DISPATCH(KERNEL, GRID, ...)                                                       \
     switch (mode) {                                                                                 \
@@ -459,6 +459,7 @@ int filter_blocks(const TilePlan& p) {
 bool dw_tiled_ok(int C) { return qt_for(C) != 0; }
 
 int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, float* Y, hipStream_t st) {
+    const unsigned tile_lds_pad = 0;
     TilePlan p = tile_plan(N, H, W, v.C);
     dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
     UNET_TILE_DISPATCH(dw_tile_fwd, grid, v, N, H, W, p.tiles_w, p.tiles_h, K, Y)
@@ -468,6 +469,7 @@ int dw_tiled_fwd(const DView& v, int mode, bool drop, int N, int H, int W, const
 
 int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, const float* K, const float* dY,
                       float* dx0, float* dx1, hipStream_t st) {
+    const unsigned tile_lds_pad = 0;
     TilePlan p = tile_plan(N, H, W, v.C);
     dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
     UNET_TILE_DISPATCH(dw_tile_bwd_data, grid, v, N, H, W, p.tiles_w, p.tiles_h, K, dY, dx0, dx1)
@@ -515,6 +517,7 @@ size_t dw_tiled_filter_partials(int N, int H, int W, int C) {
 
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st) {
+    const unsigned tile_lds_pad = (unsigned)lab_knob("UNET_DWF_LDSPAD", 0);  // lab: dynamic LDS pad (fewer blocks per CU)
     TilePlan p = tile_plan(N, H, W, v.C);
     const int G = filter_blocks(p);
     dim3 grid((unsigned)G, (unsigned)p.chunks);

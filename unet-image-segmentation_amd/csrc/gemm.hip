@@ -486,14 +486,28 @@ __device__ __forceinline__ void lab_stagger(int ko) {
         for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
 }
 #define ROWS_STAGGER(g) lab_stagger((g).ko)
+// lab: ko bit 17 = per-block stamps into lab_rows_stamps[block][4] (thread 0 only): s_memrealtime
+// (100 MHz, device-wide) at start and end, s_memtime (shader cycles, per XCD) after the prologue
+// stage and after the k-loop
+__device__ unsigned long long lab_rows_stamps[65536 * 4];
+#define ROWS_STAMP(g, i)                                                                       \
+    do {                                                                                       \
+        if (((g).ko & 0x20000) && threadIdx.x == 0) {                                          \
+            const unsigned lin_ = blockIdx.x + blockIdx.y * gridDim.x;                         \
+            if (lin_ < 65536) lab_rows_stamps[4 * lin_ + (i)] =                               \
+                ((i) == 0 || (i) == 3) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+        }                                                                                      \
+    } while (0)
 #else
 #define ROWS_STAGGER(g) ((void)0)
+#define ROWS_STAMP(g, i) ((void)0)
 #endif
 
 template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC, bool X6 = false>
 __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     main_stream_prio();
     ROWS_STAGGER(g);
+    ROWS_STAMP(g, 0);
     constexpr int LR = BK + 4;     // A (and k-contiguous B) LDS row stride, floats
     constexpr int LB = BN + 4;     // k-major B LDS row stride (n-contiguous weights)
     constexpr int XR = BK + 8;     // X6: bf16 row stride of the split planes
@@ -677,6 +691,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     load_stage(0);
     store_stage(0);
     __syncthreads();
+    ROWS_STAMP(g, 1);
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < nk) load_stage((kt + 1) * BK);
@@ -732,6 +747,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         __syncthreads();
     }
 
+    ROWS_STAMP(g, 2);
     const bool full = M_rem == BM;  // every row of the tile exists: no per-row checks
     if constexpr (EPI == E_STORE || EPI == E_STATS || EPI == E_BNPART) {
         const int ldc = (int)g.ldc;
@@ -886,6 +902,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                     if (obase[tm][r] >= 0) g.C[(int64_t)obase[tm][r] + toff] = acc[tm][tn][r] + bias;
         }
     }
+    ROWS_STAMP(g, 3);
 }
 
 // ------------------------------------------------------------- vectorised wgrad GEMM ----
@@ -1348,6 +1365,7 @@ bool rows_vec_ok(const RowsArgs& a, int amode) {
 // take BK = 32 from K = 256 on.  Lab build: UNET_ROWS_BN / UNET_ROWS_BK override (tuning only).
 struct RowsCfg {
     int bn, bk;
+    int bm = 128;
 };
 RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     const int env_bn = lab_knob("UNET_ROWS_BN", 0);
@@ -1359,6 +1377,10 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
         // lab: UNET_BNBWD_BK16 = 1 stages BK = 16 (40 KB of LDS instead of 72 KB at 128 columns:
         // co-residency with the side stream's weight-gradient blocks)
         const int bk = lab_knob("UNET_BNBWD_BK16", 0) ? 16 : 32;
+        // under-filled grids (the 16 x 16 level at batch 8): 64-row x 128-column tiles instead of
+        // 128 x 64, the same block count with half the N-tiles re-forming each dz tile
+        // (tools/lab/gemm_lab.hip LAB_BATCH=8, profiles/r5_lab/r5d_rows_b8.log: 76 -> 65.5 us)
+        if (narrow && a.N >= 128 && lab_knob("UNET_BNBWD_BM64", 1)) return RowsCfg{128, 32, 64};
         if (a.N <= 64 || narrow) return RowsCfg{64, bk};
         if (a.N >= 256 && cdiv(a.M, 128) * cdiv(a.N, 256) >= 512) return RowsCfg{256, 16};
         return RowsCfg{128, bk};
@@ -1369,11 +1391,11 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
 }
 
-template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false>
+template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false, int BM = 128>
 void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
-    dim3 grid((unsigned)cdiv(a.M, 128), (unsigned)cdiv(a.N, BN));
-    if (a.sbk == 1) gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
-    else gemm_rows_vec<128, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
+    dim3 grid((unsigned)cdiv(a.M, BM), (unsigned)cdiv(a.N, BN));
+    if (a.sbk == 1) gemm_rows_vec<BM, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
+    else gemm_rows_vec<BM, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
 }
 
 // Split-precision (bf16x6) rows / wgrad GEMMs: lab build only (UNET_X6).  Measured (tools/bench_rows.py,
@@ -1394,6 +1416,13 @@ int launch_rows(const RowsArgs& a0, hipStream_t st, const char* what) {
             return 0;
         }
 #endif
+        if constexpr (AMODE == A_BNBWD && EPI == E_STORE) {  // (the only 64-row tile: no per-128-row partials)
+            if (c.bm == 64) {
+                launch_rows_tile<128, 32, AMODE, DROP, EPI, false, 64>(a, st);
+                UNET_CHECK_LAUNCH(what);
+                return 0;
+            }
+        }
         if (c.bn == 64 && c.bk == 16) launch_rows_tile<64, 16, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 64 && c.bk == 32) launch_rows_tile<64, 32, AMODE, DROP, EPI>(a, st);
         else if (c.bn == 128 && c.bk == 32) launch_rows_tile<128, 32, AMODE, DROP, EPI>(a, st);
@@ -1444,35 +1473,36 @@ bool wgrad_x6() { return lab_knob("UNET_X6", 0) != 0; }
 template <int AMODE, bool ADROP, int BMODE, bool BDROP>
 void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
     dim3 grid((unsigned)w.tiles, (unsigned)w.S);
+    const unsigned pad = (unsigned)lab_knob("UNET_WGRAD_LDSPAD", 0);  // lab: dynamic LDS pad (fewer blocks per CU)
     const bool vec = a.P % 4 == 0 && a.Q % 4 == 0 && (AMODE != W_UNSHUFFLE || a.uf % 4 == 0) &&
                      (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
                      ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
     if (vec || BMODE == W_BNBWD) {
 #ifdef UNET_LAB_BUILD
         if (w.bp == 128 && w.bq == 128 && wgrad_x6()) {
-            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP, true><<<grid, 256, 0, st>>>(a);
+            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP, true><<<grid, 256, pad, st>>>(a);
             return;
         }
 #endif
         if (w.bp == 128 && w.bq == 128)
-            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+            gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
         else if (w.bp == 128)
-            gemm_wgrad_vec<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+            gemm_wgrad_vec<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
         else if (w.bq == 128)
-            gemm_wgrad_vec<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+            gemm_wgrad_vec<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
         else
-            gemm_wgrad_vec<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+            gemm_wgrad_vec<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
         return;
     }
     if constexpr (BMODE == W_BNBWD) return;  // (unreachable: the vectorised kernel above)
     else if (w.bp == 128 && w.bq == 128)
-        gemm_wgrad_kernel<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        gemm_wgrad_kernel<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
     else if (w.bp == 128)
-        gemm_wgrad_kernel<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        gemm_wgrad_kernel<128, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
     else if (w.bq == 128)
-        gemm_wgrad_kernel<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        gemm_wgrad_kernel<64, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
     else
-        gemm_wgrad_kernel<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, 0, st>>>(a);
+        gemm_wgrad_kernel<64, 64, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
 }
 
 // out[P][Q] (row stride ldo) = sum_m A(m, p) B(m, q)
