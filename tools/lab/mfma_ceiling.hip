@@ -89,6 +89,76 @@ __global__ __launch_bounds__(256) void mfma_k(const float* __restrict__ src, flo
     }
 }
 
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+// bf16 32x32x16 MFMA stream with NV VALU fmaf per stage (same stage structure, 12 MFMAs per stage per wave
+// = 384 cycles, the bf16x6 equivalent of 2 f32 32x32x2 k-groups x 2x2 tiles costs 6 x 4 = 24 MFMAs)
+template <int NV>
+__global__ __launch_bounds__(256) void mfma_bf16_k(const float* __restrict__ src, float* out, int iters,
+                                                   unsigned long long* stamps) {
+    __shared__ __attribute__((aligned(16))) float L[2][128 * 36 * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lo = lane & 31, hi = lane >> 5;
+    unsigned long long t0 = 0, r0 = 0;
+    if (tid == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+    for (int i = tid; i < 2 * 128 * 36 * 2; i += 256) (&L[0][0])[i] = src[(blockIdx.x * 7919 + i) & 0xFFFFF];
+    __syncthreads();
+    floatx16 acc[2][2];
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    float4 g4 = make_float4(0, 0, 0, 0);
+    for (int it = 0; it < iters; ++it) {
+        const int buf = it & 1;
+        bf16x8 fa[2], fb[2];
+        for (int t = 0; t < 2; ++t) {
+            fa[t] = *reinterpret_cast<const bf16x8*>(&L[buf][((wave >> 1) * 64 + t * 32 + lo) * 36 + 4 * hi]);
+            fb[t] = *reinterpret_cast<const bf16x8*>(&L[buf][128 * 36 + ((wave & 1) * 64 + t * 32 + lo) * 36 + 4 * hi]);
+        }
+#pragma unroll
+        for (int rep = 0; rep < 6; ++rep)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < NV / 4; ++v) {
+            g4.x = fmaf(g4.x, 1.0001f, (float)fa[0][0]);
+            g4.y = fmaf(g4.y, 1.0001f, (float)fa[0][1]);
+            g4.z = fmaf(g4.z, 1.0001f, (float)fa[1][0]);
+            g4.w = fmaf(g4.w, 1.0001f, (float)fa[1][1]);
+        }
+        __syncthreads();
+    }
+    float s = g4.x + g4.y + g4.z + g4.w;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+            for (int r = 0; r < 16; ++r) s += acc[a][b][r];
+    out[blockIdx.x * 256 + tid] = s;
+    if (tid == 0) {
+        stamps[4 * blockIdx.x + 0] = t0;
+        stamps[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
+        stamps[4 * blockIdx.x + 2] = r0;
+        stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+template <int NV>
+static void run_bf16(const char* name, const float* src, float* out, unsigned long long* st, int blocks, int iters) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    for (int w = 0; w < 20; ++w) mfma_bf16_k<NV><<<blocks, 256>>>(src, out, iters, st);
+    CK(hipEventRecord(a));
+    const int reps = 10;
+    for (int w = 0; w < reps; ++w) mfma_bf16_k<NV><<<blocks, 256>>>(src, out, iters, st);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    const double us = ms * 1e3 / reps;
+    const double mf = (double)blocks * 4 * iters * 24;  // MFMAs
+    const double cyc_per_mfma = us * 1e-6 * 2.39e9 / (mf / 1024.0);  // per SIMD
+    printf("%-34s %9.1f us  %.1f cycles per bf16 MFMA per SIMD (32 = back-to-back)\n", name, us, cyc_per_mfma);
+}
+
 template <int MODE>
 static void run(const char* name, const float* src, float* out, unsigned long long* st, int blocks, int iters) {
     hipEvent_t a, b;
@@ -134,5 +204,9 @@ int main() {
     run<3>("mode 3, 32 stages (K=512 at BK16)", src, out, st, blocks, 32);
     run<6>("mode 6, 32 stages", src, out, st, blocks, 32);
     run<0>("registers only (again)", src, out, st, blocks, iters);
+    run_bf16<0>("bf16 MFMA + LDS frags + barrier", src, out, st, blocks, iters);
+    run_bf16<64>("bf16 + 64 VALU / stage", src, out, st, blocks, iters);
+    run_bf16<128>("bf16 + 128 VALU / stage", src, out, st, blocks, iters);
+    run_bf16<256>("bf16 + 256 VALU / stage", src, out, st, blocks, iters);
     return 0;
 }

@@ -1459,7 +1459,7 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     int target = lab_knob("UNET_WGRAD_BLOCKS", 1024);  // ~4 blocks per CU
     if (target < 1) target = 1024;
     int64_t want = cdiv(target, w.tiles);
-    int64_t maxs = M / 512;               // >= 32 k-steps per block: fewer, cheaper slabs
+    int64_t maxs = M / lab_knob("UNET_WGRAD_MINROWS", 512);  // >= 32 k-steps per block: fewer, cheaper slabs
     if (maxs < 1) maxs = 1;
     int64_t S = want < maxs ? want : maxs;
     if (S < 1) S = 1;
