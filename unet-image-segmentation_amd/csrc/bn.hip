@@ -427,6 +427,7 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
 // (left zero on exit).
 int bwd_stats_finish(const float* part, int S, int c, int64_t m, int use_bn, const float* mean, const float* rstd,
                      float* dgamma, float* dbeta, float* coef, double* scratch, unsigned* cnt, hipStream_t st) {
+    if (lab_knob("UNET_SKIP_BNBWD", 0)) return 0;  // lab: upper bound of folding the launch away
     const unsigned gx = (unsigned)cdiv(c / 4, kLQ);
     const unsigned nch = S <= kGroupSlabs ? 1u : (unsigned)cdiv(S, kGroupSlabs);
     bn_bwd_stats_kernel<<<dim3(gx, nch), 256, 0, st>>>(part, S, c, m, use_bn, mean, rstd, dgamma, dbeta, coef, scratch,
@@ -511,6 +512,7 @@ extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const floa
     UNET_CHECK_ARG(bn_partials && scale && shift && m > 0 && c > 0, "unet_bn_finalize: bad args");
     UNET_CHECK_ARG(!gamma || beta, "unet_bn_finalize: gamma without beta");
     hipStream_t st = as_stream(stream);
+    if (lab_knob("UNET_SKIP_BNFIN", 0)) return 0;  // lab: upper bound of folding the launch away
     const int64_t nblk = cdiv(m, kStatsRows);
     const int nch = (int)cdiv(nblk, kChunkParts);
     const float2* part = reinterpret_cast<const float2*>(bn_partials);
