@@ -294,6 +294,8 @@ def main():
                     help="128-output blocks too: no y store, weight gradients recompute it (A/B)")
     ap.add_argument("--recompute-y64-128", action="store_true",
                     help="the 64 -> 128 block (enc2_block1) too: no y store, recomputed (A/B)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="data parallel: BatchNorm over the global batch (SyncBN) instead of per replica")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
     args = ap.parse_args()
@@ -323,7 +325,7 @@ def main():
     model.compile(AdamW(learning_rate=2e-3, weight_decay=1e-4), "dice_loss",
                   metrics=[MeanIoU(num_classes=2, name="mean_io_u", device=device), "dice_coef"])
     if world > 1:
-        model.enable_data_parallel()
+        model.enable_data_parallel(sync_bn=args.sync_bn)
     model.engine.use_x3 = not args.no_x3
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
@@ -430,7 +432,8 @@ def main():
                                    f"step (fwd + dice_loss + bwd + AdamW + MeanIoU(2) update, dropout 0.2)",
                        "network": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                       "seq_len": args.size * args.size, "parallelism": f"dp{world}"},
+                       "seq_len": args.size * args.size, "parallelism": f"dp{world}",
+                       "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-replica"},
             "final_loss": round(loss, 6),
         }
         if timer is not None:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 10
+#define UNET_ABI_VERSION 11
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -255,6 +255,25 @@ int unet_bn_finalize(float* bn_partials, int64_t m, int c,
                      float momentum, float* moving_mean, float* moving_var,
                      int update_moving, float* mean, float* rstd,
                      float* scale, float* shift, unet_stream_t stream);
+/* SyncBN under data parallelism (SURVEY §8(e) option; off by default: the reference's
+ * tf.distribute default, and Keras BatchNormalization(synchronized=False), normalise each
+ * replica over its own shard).  unet_bn_moments reduces this replica's partials (as
+ * unet_bn_finalize does, same counters) to a record of 1 + 2c doubles: (count, mean[c], M2[c]);
+ * the caller gathers the replicas' records ([world][1 + 2c], rank order) and
+ * unet_bn_finalize_moments combines them in rank order (Chan's parallel formula, double) and
+ * finalizes exactly as unet_bn_finalize with the global-batch mean / biased variance.  Every
+ * replica combining the same gathered records ends with identical statistics.
+ * Backward: unet_bn_bwd_coef forms coef = (mean, S1/m, rstd*S2/m) from the all-reduced sums
+ * sums[0..c) = sum g, sums[c..2c) = sum g*xhat over all replicas (m = the global pixel count);
+ * the replica's own dgamma / dbeta stay its local sums (the gradient all-reduce averages them). */
+int unet_bn_moments(float* bn_partials, int64_t m, int c, double* moments, unet_stream_t stream);
+int unet_bn_finalize_moments(const double* moments, int world, int c, const float* gamma,
+                             const float* beta, float eps, float momentum, float* moving_mean,
+                             float* moving_var, int update_moving, float* mean, float* rstd,
+                             float* scale, float* shift, unet_stream_t stream);
+int unet_bn_bwd_coef(const float* sums, int64_t m, int c, int use_bn, const float* mean,
+                     const float* rstd, float* coef, unet_stream_t stream);
+
 /* Inference: scale/shift from the moving statistics. */
 int unet_bn_infer_params(const float* gamma, const float* beta,
                          const float* moving_mean, const float* moving_var,

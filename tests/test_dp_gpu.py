@@ -43,6 +43,26 @@ def test_dp_two_ranks_equal_weighted_single_process(global_batch, deferred):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("global_batch", [4, 5])
+def test_dp_sync_bn_equals_full_batch(global_batch):
+    """tools/dp_syncbn_check.py: with SyncBN (model.enable_data_parallel(sync_bn=True), SURVEY 8(e)
+    option) a two-rank step over shards 2+2 / 3+2 equals ONE single-process step over the whole
+    global batch (dropout off): gradients within fp32 reduction order, moving statistics equal,
+    and every rank bitwise identical."""
+    env = dict(os.environ)
+    env["DP_CHECK_GLOBAL"] = str(global_batch)
+    if torch.cuda.device_count() < 2:
+        env["UNET_DP_ONE_DEVICE"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tools", "dp_syncbn_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "identical across ranks: True" in r.stdout
+    assert r.stdout.count("equal to full batch: True") == 2, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
 def test_bench_gpus_flag_spawns_ranks():
     """`python bench.py --gpus 2` (the driver's command shape, no launcher environment) runs two
     ranks: the parent starts torch.distributed.run as a child before touching the GPU, and the

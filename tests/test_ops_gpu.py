@@ -158,6 +158,54 @@ def test_pointwise_and_bn_stats(ops, m, cin, cout, off):
     assert torch.equal(z, z2)
 
 
+@pytest.mark.parametrize("rows,cout,off", [((3000, 2000), 64, 0.0), ((24653, 9000), 128, 25.0),
+                                           ((128, 129, 1000), 96, 1.0), ((5000,), 256, 0.0)])
+def test_bn_sync_moments(ops, rows, cout, off):
+    """SyncBN forward (unet_bn_moments + unet_bn_finalize_moments): the replicas' records combined in
+    rank order give the statistics of the concatenated batch -- against unet_bn_finalize over all
+    rows and the float64 oracle; one replica reproduces unet_bn_finalize.  Backward coefficients
+    (unet_bn_bwd_coef) = (mean, S1 / m, rstd S2 / m)."""
+    rng = np.random.default_rng(sum(rows) + cout)
+    cin = 32
+    pk = f32(rng.standard_normal((1, 1, cin, cout)) / np.sqrt(cin))
+    ys = [f32(rng.standard_normal((r, cin)) + off) for r in rows]
+    gamma, beta = bn_affine(rng, cout)
+    mm = f32(rng.standard_normal(cout) * 0.1)
+    mv = f32(1 + rng.random(cout))
+    R = 1 + 2 * cout
+    recs = torch.empty(len(rows) * R, dtype=torch.float64, device="cuda")
+    for i, (r, y) in enumerate(zip(rows, ys)):
+        z = torch.empty((r, cout), device="cuda")
+        part = torch.zeros(ops.bn_partials_numel(r, cout), device="cuda")
+        ops.pointwise_fwd(dev(y), r, cin, cout, dev(pk), z, part)
+        ops.bn_moments(part, r, cout, recs[i * R:(i + 1) * R])
+    tm, tv = dev(mm), dev(mv)
+    outs = [torch.empty(cout, device="cuda") for _ in range(4)]
+    ops.bn_finalize_moments(recs, len(rows), cout, dev(gamma), dev(beta), 1e-3, 0.99, tm, tv, True, *outs)
+    # reference: one replica holding every row
+    M = sum(rows)
+    yall = np.concatenate(ys)
+    zall = torch.empty((M, cout), device="cuda")
+    pall = torch.zeros(ops.bn_partials_numel(M, cout), device="cuda")
+    ops.pointwise_fwd(dev(yall), M, cin, cout, dev(pk), zall, pall)
+    tm2, tv2 = dev(mm), dev(mv)
+    ref = [torch.empty(cout, device="cuda") for _ in range(4)]
+    ops.bn_finalize(pall, M, cout, dev(gamma), dev(beta), 1e-3, 0.99, tm2, tv2, True, *ref)
+    for a, b in zip(outs + [tm, tv], ref + [tm2, tv2]):
+        assert rel_err(host(a), host(b)) < 2e-6
+    zr = (yall @ pk[0, 0]).reshape(M, 1, 1, cout)
+    _, mean, var = K.bn_train(zr, gamma, beta)
+    assert rel_err(host(outs[0]), mean) < 1e-4
+    assert rel_err(host(outs[1]), 1 / np.sqrt(var + 1e-3)) < 1e-5
+    # backward coefficients from (all-reduced) sums
+    sums = dev(f32(rng.standard_normal(2 * cout)))
+    coef = torch.empty(3 * cout, device="cuda")
+    ops.bn_bwd_coef(sums, M, cout, True, outs[0], outs[1], coef)
+    sh = host(sums)
+    want = np.concatenate([host(outs[0]), sh[:cout] / M, host(outs[1]) * (sh[cout:] / M)])
+    assert rel_err(host(coef), want) < 1e-6
+
+
 @pytest.mark.parametrize("m,cin,cout", [(100, 3, 64), (256, 64, 64), (300, 128, 64), (200, 256, 512),
                                         (64, 1024, 1024)])
 def test_pointwise_bwd(ops, m, cin, cout):

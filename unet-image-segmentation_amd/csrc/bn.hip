@@ -40,6 +40,12 @@ __device__ __forceinline__ void chunk_sums(const float2* __restrict__ part, int6
     }
 }
 
+__device__ __forceinline__ void bn_apply_channel(int c, float mean, float var, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float eps, float momentum,
+                                                 float* moving_mean, float* moving_var, int update_moving,
+                                                 float* mean_out, float* rstd_out, float* scale_out,
+                                                 float* shift_out);
+
 // Pass 2 (same launch, lastblock.h): every block publishes its chunk row (sc1 stores); the last
 // block of each 64-channel column to arrive sums the rows (4 lanes over interleaved chunks,
 // combined in lane order) -> mean, biased var, folded affine, moving update.  One chunk: the
@@ -54,6 +60,16 @@ __device__ __forceinline__ void bn_finalize_channel(int c, double s1, double s2,
     const float mean = (float)((double)part[c].x + dm);
     double vd = s2 / (double)M - dm * dm;
     const float var = (float)(vd > 0.0 ? vd : 0.0);
+    bn_apply_channel(c, mean, var, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving, mean_out,
+                     rstd_out, scale_out, shift_out);
+}
+
+// the batch (mean, biased var) of channel c -> rstd, the folded affine, the moving update
+__device__ __forceinline__ void bn_apply_channel(int c, float mean, float var, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float eps, float momentum,
+                                                 float* moving_mean, float* moving_var, int update_moving,
+                                                 float* mean_out, float* rstd_out, float* scale_out,
+                                                 float* shift_out) {
     const float rstd = 1.0f / sqrtf(var + eps);
     if (gamma) {
         const float sc = gamma[c] * rstd;
@@ -77,7 +93,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
                                                           const float* __restrict__ beta, float eps, float momentum,
                                                           float* moving_mean, float* moving_var, int update_moving,
                                                           float* mean_out, float* rstd_out, float* scale_out,
-                                                          float* shift_out) {
+                                                          float* shift_out, double* moments) {
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const int lane = threadIdx.x >> 6;
     const int nch = gridDim.y;
@@ -119,8 +135,39 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
             }
     }
     if (lane != 0 || c >= C) return;
+    if (moments) {  // SyncBN: this replica's (count, mean, M2) for the cross-replica combine
+        if (c == 0) moments[0] = (double)M;
+        moments[1 + c] = (double)part[c].x + s1 / (double)M;
+        moments[1 + C + c] = s2 - s1 * (s1 / (double)M);
+        return;
+    }
     bn_finalize_channel(c, s1, s2, part, M, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving,
                         mean_out, rstd_out, scale_out, shift_out);
+}
+
+// SyncBN: the replicas' records [world][1 + 2C] = (count, mean[C], M2[C]) combined in rank order
+// (Chan's parallel formula, double; every replica runs the same order on the same gathered records,
+// so all end bitwise identical), then the finalize of the global-batch statistics.
+__global__ void bn_finalize_moments_kernel(const double* __restrict__ recs, int world, int C,
+                                           const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                           float momentum, float* moving_mean, float* moving_var, int update_moving,
+                                           float* mean_out, float* rstd_out, float* scale_out, float* shift_out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int64_t R = 1 + 2 * (int64_t)C;
+    double n = recs[0], mu = recs[1 + c], m2 = recs[1 + C + c];
+    for (int r = 1; r < world; ++r) {
+        const double nr = recs[r * R], mr = recs[r * R + 1 + c], m2r = recs[r * R + 1 + C + c];
+        const double nt = n + nr;
+        if (nr <= 0.0) continue;
+        const double d = mr - mu;
+        mu += d * (nr / nt);
+        m2 += m2r + d * d * (n * nr / nt);
+        n = nt;
+    }
+    const double vd = m2 / n;
+    bn_apply_channel(c, (float)mu, (float)(vd > 0.0 ? vd : 0.0), gamma, beta, eps, momentum, moving_mean, moving_var,
+                     update_moving, mean_out, rstd_out, scale_out, shift_out);
 }
 
 __global__ void bn_infer_kernel(const float* gamma, const float* beta, const float* mm, const float* mv, int C,
@@ -523,8 +570,48 @@ extern "C" int unet_bn_finalize(float* bn_partials, int64_t m, int c, const floa
                                                 align_up((size_t)nch * c * sizeof(double2), 256));
     bn_finalize_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, st>>>(
         part, nblk, m, c, chunks, cnt, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving, mean, rstd,
-        scale, shift);
+        scale, shift, nullptr);
     UNET_CHECK_LAUNCH("unet_bn_finalize");
+    return 0;
+}
+
+extern "C" int unet_bn_moments(float* bn_partials, int64_t m, int c, double* moments, unet_stream_t stream) {
+    UNET_CHECK_ARG(bn_partials && moments && m > 0 && c > 0, "unet_bn_moments: bad args");
+    const int64_t nblk = cdiv(m, kStatsRows);
+    const int nch = (int)cdiv(nblk, kChunkParts);
+    const float2* part = reinterpret_cast<const float2*>(bn_partials);
+    double* chunks = reinterpret_cast<double*>(reinterpret_cast<char*>(bn_partials) +
+                                               align_up((size_t)nblk * c * sizeof(float2), 256));
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(bn_partials) +
+                                                align_up((size_t)nblk * c * sizeof(float2), 256) +
+                                                align_up((size_t)nch * c * sizeof(double2), 256));
+    bn_finalize_kernel<<<dim3((unsigned)cdiv(c, 64), (unsigned)nch), 256, 0, as_stream(stream)>>>(
+        part, nblk, m, c, chunks, cnt, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+        nullptr, moments);
+    UNET_CHECK_LAUNCH("unet_bn_moments");
+    return 0;
+}
+
+extern "C" int unet_bn_finalize_moments(const double* moments, int world, int c, const float* gamma,
+                                        const float* beta, float eps, float momentum, float* moving_mean,
+                                        float* moving_var, int update_moving, float* mean, float* rstd, float* scale,
+                                        float* shift, unet_stream_t stream) {
+    UNET_CHECK_ARG(moments && world > 0 && c > 0 && scale && shift, "unet_bn_finalize_moments: bad args");
+    UNET_CHECK_ARG(!gamma || beta, "unet_bn_finalize_moments: gamma without beta");
+    bn_finalize_moments_kernel<<<(unsigned)cdiv(c, 256), 256, 0, as_stream(stream)>>>(
+        moments, world, c, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving, mean, rstd, scale,
+        shift);
+    UNET_CHECK_LAUNCH("unet_bn_finalize_moments");
+    return 0;
+}
+
+extern "C" int unet_bn_bwd_coef(const float* sums, int64_t m, int c, int use_bn, const float* mean,
+                                const float* rstd, float* coef, unet_stream_t stream) {
+    UNET_CHECK_ARG(sums && coef && m > 0 && c > 0, "unet_bn_bwd_coef: bad args");
+    UNET_CHECK_ARG(!use_bn || (mean && rstd), "unet_bn_bwd_coef: use_bn needs mean/rstd");
+    bn_bwd_coef_kernel<<<(unsigned)cdiv(c, 256), 256, 0, as_stream(stream)>>>(sums, c, m, use_bn, mean, rstd, nullptr,
+                                                                               nullptr, coef);
+    UNET_CHECK_LAUNCH("unet_bn_bwd_coef");
     return 0;
 }
 

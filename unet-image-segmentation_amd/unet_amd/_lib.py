@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -71,6 +71,9 @@ SIGNATURES = {
                                        c_size_t, P]),
     "unet_sepconv_set_schedule": (c_int, [c_int]),
     "unet_bn_finalize": (c_int, [P, c_int64, c_int, P, P, c_float, c_float, P, P, c_int, P, P, P, P, P]),
+    "unet_bn_moments": (c_int, [P, c_int64, c_int, P, P]),
+    "unet_bn_finalize_moments": (c_int, [P, c_int, c_int, P, P, c_float, c_float, P, P, c_int, P, P, P, P, P]),
+    "unet_bn_bwd_coef": (c_int, [P, c_int64, c_int, c_int, P, P, P, P]),
     "unet_bn_infer_params": (c_int, [P, P, P, P, c_int, c_float, P, P, P]),
     "unet_bn_relu_bwd_workspace": (c_size_t, [c_int64, c_int]),
     "unet_bn_relu_bwd": (c_int, [P, P, c_int64, c_int, P, P, P, P, c_int, c_float, c_uint64, P, P, P, P,

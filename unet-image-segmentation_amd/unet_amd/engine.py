@@ -97,6 +97,9 @@ class BlockBufs:
     zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
     dlogit: Optional[torch.Tensor] = None  # last block, binary head: dL/dlogit per pixel (its da is rank one)
     da_rank1: bool = False  # this backward's da is dlogit (x) the head kernel, never materialised
+    rec: Optional[torch.Tensor] = None  # SyncBN: this replica's (count, mean, M2) record, float64 1 + 2C
+    recs: Optional[torch.Tensor] = None  # SyncBN: the gathered records [world][1 + 2C]
+    bsums: Optional[torch.Tensor] = None  # SyncBN backward: [sum g | sum g*xhat] (2C), all-reduced
 
 
 @dataclass
@@ -196,6 +199,14 @@ class UNetEngine:
         # weight gradients from it; dz never stored) instead of the data-gradient GEMM + the
         # side-stream weight-gradient pass
         self.fuse_block_bwd = True
+        # SyncBN (SURVEY 8(e) option, off by default like tf.distribute / Keras synchronized=False):
+        # under data parallelism every BatchNorm uses the global batch's statistics -- the forward
+        # gathers each replica's (count, mean, M2) and combines them in rank order, the backward
+        # all-reduces (sum g, sum g*xhat) before dz is formed.  Set by model.enable_data_parallel.
+        self.sync_bn = False
+        self.sync_group = None
+        self.sync_world = 1
+        self.sync_global_n = 0  # images in the global batch of the current step (model.train_step)
         self._pending_side = None
         self._pending_ready: Optional[str] = None
         self._ev = None  # created on first use (on the device)
@@ -340,8 +351,7 @@ class UNetEngine:
             ops.sepconv_fwd(view, n, h, w, dk, b.cout, pk, bb.y if keep_y else None, bb.z,
                             bb.part if stats else None, bb.zsel, gamma, self._pkx(b))
             if stats:
-                ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean,
-                                bb.rstd, bb.scale, bb.shift)
+                self._bn_finalize(bb, m, b.cout, gamma, beta, mm, mv)
             else:
                 ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
             return View.bnrelu(bb.z, bb.scale, bb.shift)
@@ -354,11 +364,42 @@ class UNetEngine:
         if bb.zsel is not None:
             ops.pool_select(bb.z, n, h, w, b.cout, gamma, bb.zsel)
         if training and self.use_bn:
-            ops.bn_finalize(bb.part, m, b.cout, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
-                            bb.scale, bb.shift)
+            self._bn_finalize(bb, m, b.cout, gamma, beta, mm, mv)
         else:
             ops.bn_infer_params(gamma, beta, mm, mv, b.cout, BN_EPS, bb.scale, bb.shift)
         return View.bnrelu(bb.z, bb.scale, bb.shift)
+
+    def _sync_bn_on(self) -> bool:
+        return self.sync_bn and self.sync_world > 1 and self.use_bn
+
+    def _bn_finalize(self, bb: BlockBufs, m: int, c: int, gamma, beta, mm, mv):
+        """The training BatchNorm statistics of a block from its producer's partials: this replica's
+        batch (unet_bn_finalize), or with SyncBN the global batch (records gathered over the group
+        and combined in rank order on every replica: unet_bn_moments / unet_bn_finalize_moments)."""
+        if not self._sync_bn_on():
+            ops.bn_finalize(bb.part, m, c, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True, bb.mean, bb.rstd,
+                            bb.scale, bb.shift)
+            return
+        import torch.distributed as dist
+        if bb.rec is None or bb.rec.numel() != 1 + 2 * c:
+            bb.rec = torch.empty(1 + 2 * c, dtype=torch.float64, device=self.device)
+            bb.recs = torch.empty(self.sync_world * (1 + 2 * c), dtype=torch.float64, device=self.device)
+        ops.bn_moments(bb.part, m, c, bb.rec)
+        dist.all_gather_into_tensor(bb.recs, bb.rec, group=self.sync_group)
+        ops.bn_finalize_moments(bb.recs, self.sync_world, c, gamma, beta, BN_EPS, BN_MOMENTUM, mm, mv, True,
+                                bb.mean, bb.rstd, bb.scale, bb.shift)
+
+    def _sync_bn_coef(self, bb: BlockBufs, b: Block, h: int, w: int, dgamma, dbeta):
+        """SyncBN backward: coef from the group's (sum g, sum g*xhat) over the global batch; the
+        replica's own dgamma / dbeta (its local sums) are left for the gradient all-reduce."""
+        import torch.distributed as dist
+        c = b.cout
+        if bb.bsums is None:
+            bb.bsums = torch.empty(2 * c, dtype=torch.float32, device=self.device)
+        ops.copy_strided(dbeta, 1, c, c, bb.bsums, c)
+        ops.copy_strided(dgamma, 1, c, c, bb.bsums[c:], c)
+        dist.all_reduce(bb.bsums, group=self.sync_group)
+        ops.bn_bwd_coef(bb.bsums, self.sync_global_n * h * w, c, True, bb.mean, bb.rstd, bb.coef)
 
     def _wts(self, b: Block, refresh: bool = True):
         """(depthwise, pointwise) kernels of a block as the kernels see them.  refresh=False (the
@@ -566,6 +607,8 @@ class UNetEngine:
                                       drop_rate, drop_seed, dgamma, dbeta, bb.coef)
             bb.bn_slabs = 0
             bb.bn_masked = False
+            if self._sync_bn_on():
+                self._sync_bn_coef(bb, b, h, w, dgamma, dbeta)
             self._flush_side()
             img_wg = self.img_fused_wgrad and drop_rate == 0.0 and b.cin == 4 and b.cout in (32, 64)
             img_all = (img_wg and self.img_fused_dwf and dx0 is None and view_f.mode == L.VIEW_PLAIN
@@ -591,6 +634,8 @@ class UNetEngine:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, dz)
         else:
+            if self._sync_bn_on():
+                raise RuntimeError("SyncBN needs the fused BN-backward route (fuse_bn_bwd, channels % 4 == 0)")
             ops.bn_relu_bwd(bb.da, bb.z, m, b.cout, bb.mean, bb.rstd, bb.scale, bb.shift, self.use_bn, drop_rate,
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)

@@ -72,12 +72,17 @@ class UNetModel:
                     raise ValueError(f"unsupported metric {m!r}")
                 self.metric_names.append(nm)
 
-    def enable_data_parallel(self, bucket_bytes: int = 6 << 20, group=None):
-        """Average gradients over torch.distributed ranks each step (bucketed, overlapped)."""
+    def enable_data_parallel(self, bucket_bytes: int = 6 << 20, group=None, sync_bn: bool = False):
+        """Average gradients over torch.distributed ranks each step (bucketed, overlapped).
+        sync_bn: BatchNorm over the global batch (SyncBN, SURVEY 8(e) option) instead of each
+        replica's shard (the reference's tf.distribute default, synchronized=False)."""
         import torch.distributed as dist
         self.bucketer = GradBucketer(self.engine.grads, bucket_bytes, group)
         self.engine.grad_hook = self.bucketer.ready
         self.engine.rank_salt = dist.get_rank(group) if dist.is_initialized() else 0
+        self.engine.sync_bn = bool(sync_bn)
+        self.engine.sync_group = group
+        self.engine.sync_world = self.bucketer.world
 
     def train_step(self, x, y, global_size: Optional[int] = None) -> torch.Tensor:
         """One optimisation step; returns the device vector [loss, dice_coef, iou_coef] of this
@@ -98,6 +103,7 @@ class UNetModel:
             if n_global < world or n_local < 1:
                 raise ValueError(f"shard of {n_local} from a global batch of {n_global} over {world} ranks")
             loss_scale = n_local * world / n_global
+            self.engine.sync_global_n = n_global
         caller = torch.cuda.current_stream(self.engine.device)
         main = self.engine.main
         main.wait_stream(caller)

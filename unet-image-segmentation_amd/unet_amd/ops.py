@@ -460,6 +460,32 @@ def bn_finalize(partials: Tensor, m: int, c: int, gamma, beta, eps, momentum, mo
            _ptr(shift), _stream())
 
 
+def bn_moments(partials: Tensor, m: int, c: int, out: Tensor):
+    """SyncBN: this replica's record (count, mean[c], M2[c]) as 1 + 2c float64 (unet_bn_moments)."""
+    _check(partials, "bn_partials", bn_partials_numel(m, c))
+    if out.dtype != torch.float64 or out.numel() < 1 + 2 * c or not out.is_cuda:
+        raise ValueError("bn_moments: out must be a float64 device tensor of 1 + 2c elements")
+    _call("unet_bn_moments", (0.0, 8.0 * bn_partials_numel(m, c) / 2), _ptr(partials), m, c, _ptr(out), _stream())
+
+
+def bn_finalize_moments(records: Tensor, world: int, c: int, gamma, beta, eps, momentum, moving_mean, moving_var,
+                        update_moving: bool, mean, rstd, scale, shift):
+    """SyncBN: the gathered records [world][1 + 2c] combined in rank order, then finalized."""
+    if records.dtype != torch.float64 or records.numel() < world * (1 + 2 * c) or not records.is_cuda:
+        raise ValueError("bn_finalize_moments: records must be float64 [world][1 + 2c] on the device")
+    _call("unet_bn_finalize_moments", (0.0, 8.0 * world * (1 + 2 * c)), _ptr(records), world, c, _ptr(gamma),
+          _ptr(beta), float(eps), float(momentum), _ptr(moving_mean), _ptr(moving_var), int(bool(update_moving)),
+          _ptr(mean), _ptr(rstd), _ptr(scale), _ptr(shift), _stream())
+
+
+def bn_bwd_coef(sums: Tensor, m: int, c: int, use_bn: bool, mean, rstd, coef: Tensor):
+    """SyncBN backward: coef (3c) from the all-reduced [sum g | sum g*xhat] (2c) over m pixels."""
+    _check(sums, "sums", 2 * c)
+    _check(coef, "coef", 3 * c)
+    _call("unet_bn_bwd_coef", (0.0, 24.0 * c), _ptr(sums), m, c, int(bool(use_bn)), _ptr(mean), _ptr(rstd),
+          _ptr(coef), _stream())
+
+
 def bn_infer_params(gamma, beta, moving_mean, moving_var, c: int, eps, scale: Tensor, shift: Tensor):
     _call("unet_bn_infer_params", (0.0, 24.0 * c), _ptr(gamma), _ptr(beta), _ptr(moving_mean), _ptr(moving_var), c, float(eps),
            _ptr(scale), _ptr(shift), _stream())
