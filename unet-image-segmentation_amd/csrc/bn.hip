@@ -21,21 +21,35 @@ constexpr int kStatsRows = 128;
 // Coalesced: consecutive threads read consecutive channels of one partial row.
 constexpr int kChunkParts = 64;
 __device__ __forceinline__ void chunk_sums(const float2* __restrict__ part, int64_t nblk, int64_t M, int C, int c,
-                                           int lane, int chunk, double& s1, double& s2) {
+                                           int lane, int chunk, double& s1, double& s2, float& k_out) {
     const int64_t b0 = (int64_t)chunk * kChunkParts;
     const int64_t b1 = b0 + kChunkParts < nblk ? b0 + kChunkParts : nblk;
     s1 = 0.0;
     s2 = 0.0;
     if (c < C) {
-        const double K = (double)part[c].x;
-#pragma unroll 4
-        for (int64_t b = b0 + lane; b < b1; b += 4) {
-            const float2 pm = part[b * C + c];
-            const int64_t rows = (M - b * kStatsRows) < kStatsRows ? (M - b * kStatsRows) : kStatsRows;
-            const double d = (double)pm.x - K;
-            const double nd = (double)rows * d;
-            s1 += nd;
-            s2 += (double)pm.y + nd * d;
+        // every load of the lane (K and its 16 partials) in flight at once: the finish is a chain of
+        // dependent round trips on the critical path, so each batch saved is ~1 us per launch
+        constexpr int PER = kChunkParts / 4;
+        const float2 k0 = part[c];
+        float2 pv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {  // branch-free: a clamped row past the chunk, masked below
+            const int64_t b = b0 + lane + 4 * i;
+            pv[i] = part[(b < b1 ? b : b0) * C + c];
+        }
+        k_out = k0.x;
+        const double K = (double)k0.x;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int64_t b = b0 + lane + 4 * i;
+            if (b < b1) {
+                const float2 pm = pv[i];
+                const int64_t rows = (M - b * kStatsRows) < kStatsRows ? (M - b * kStatsRows) : kStatsRows;
+                const double d = (double)pm.x - K;
+                const double nd = (double)rows * d;
+                s1 += nd;
+                s2 += (double)pm.y + nd * d;
+            }
         }
     }
 }
@@ -50,20 +64,6 @@ __device__ __forceinline__ void bn_apply_channel(int c, float mean, float var, c
 // block of each 64-channel column to arrive sums the rows (4 lanes over interleaved chunks,
 // combined in lane order) -> mean, biased var, folded affine, moving update.  One chunk: the
 // block's own sums are final.
-__device__ __forceinline__ void bn_finalize_channel(int c, double s1, double s2, const float2* __restrict__ part,
-                                                    int64_t M, const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, float eps, float momentum,
-                                                    float* moving_mean, float* moving_var, int update_moving,
-                                                    float* mean_out, float* rstd_out, float* scale_out,
-                                                    float* shift_out) {
-    const double dm = s1 / (double)M;
-    const float mean = (float)((double)part[c].x + dm);
-    double vd = s2 / (double)M - dm * dm;
-    const float var = (float)(vd > 0.0 ? vd : 0.0);
-    bn_apply_channel(c, mean, var, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving, mean_out,
-                     rstd_out, scale_out, shift_out);
-}
-
 // the batch (mean, biased var) of channel c -> rstd, the folded affine, the moving update
 __device__ __forceinline__ void bn_apply_channel(int c, float mean, float var, const float* __restrict__ gamma,
                                                  const float* __restrict__ beta, float eps, float momentum,
@@ -95,10 +95,22 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
                                                           float* mean_out, float* rstd_out, float* scale_out,
                                                           float* shift_out, double* moments) {
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int lane = threadIdx.x >> 6;
+    const int lane = threadIdx.x >> 6;  // = the wave: lane 0 is wave 0, which finalizes
     const int nch = gridDim.y;
+    // the finalize's other inputs loaded up front, beside the chunk's partials (its own round trips
+    // would otherwise follow the reduction's)
+    float gv = 1.f, bv = 0.f, mmv = 0.f, mvv = 0.f;
+    if (lane == 0 && c < C && !moments) {
+        if (gamma) gv = gamma[c];
+        if (beta) bv = beta[c];
+        if (update_moving && moving_mean && moving_var) {
+            mmv = moving_mean[c];
+            mvv = moving_var[c];
+        }
+    }
     double s1, s2;
-    chunk_sums(part, nblk, M, C, c, lane, blockIdx.y, s1, s2);
+    float K = 0.f;  // mean of partial 0 (the shift)
+    chunk_sums(part, nblk, M, C, c, lane, blockIdx.y, s1, s2, K);
     __shared__ double r1[256], r2[256];
     __shared__ int flag;
     r1[threadIdx.x] = s1;
@@ -118,10 +130,21 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
         s1 = 0.0;
         s2 = 0.0;
         if (c < C) {
-#pragma unroll 8
-            for (int k = lane; k < nch; k += 4) {
-                s1 += ld_agent(chunks + ((int64_t)k * C + c) * 2);
-                s2 += ld_agent(chunks + ((int64_t)k * C + c) * 2 + 1);
+            constexpr int FB = 16;  // chunk rows per lane in flight at once (same order of the sums)
+            for (int k0 = lane; k0 < nch; k0 += 4 * FB) {
+                double a1[FB], a2[FB];
+#pragma unroll
+                for (int i = 0; i < FB; ++i) {
+                    const int k = k0 + 4 * i;
+                    a1[i] = k < nch ? ld_agent(chunks + ((int64_t)k * C + c) * 2) : 0.0;
+                    a2[i] = k < nch ? ld_agent(chunks + ((int64_t)k * C + c) * 2 + 1) : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < FB; ++i)
+                    if (k0 + 4 * i < nch) {
+                        s1 += a1[i];
+                        s2 += a2[i];
+                    }
             }
         }
         __syncthreads();  // r1/r2 were read above by lane 0 before the arrival barrier; reuse
@@ -137,12 +160,29 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float2* __restri
     if (lane != 0 || c >= C) return;
     if (moments) {  // SyncBN: this replica's (count, mean, M2) for the cross-replica combine
         if (c == 0) moments[0] = (double)M;
-        moments[1 + c] = (double)part[c].x + s1 / (double)M;
+        moments[1 + c] = (double)K + s1 / (double)M;
         moments[1 + C + c] = s2 - s1 * (s1 / (double)M);
         return;
     }
-    bn_finalize_channel(c, s1, s2, part, M, gamma, beta, eps, momentum, moving_mean, moving_var, update_moving,
-                        mean_out, rstd_out, scale_out, shift_out);
+    const double dm = s1 / (double)M;
+    const float mean = (float)((double)K + dm);
+    double vd = s2 / (double)M - dm * dm;
+    const float var = (float)(vd > 0.0 ? vd : 0.0);
+    const float rstd = 1.0f / sqrtf(var + eps);
+    if (gamma) {
+        const float sc = gv * rstd;
+        scale_out[c] = sc;
+        shift_out[c] = bv - mean * sc;
+    } else {  // use_batch_norm=False: relu(z + bias)
+        scale_out[c] = 1.0f;
+        shift_out[c] = beta ? bv : 0.f;
+    }
+    if (mean_out) mean_out[c] = mean;
+    if (rstd_out) rstd_out[c] = rstd;
+    if (update_moving && moving_mean && moving_var) {
+        moving_mean[c] = mmv * momentum + mean * (1.0f - momentum);
+        moving_var[c] = mvv * momentum + var * (1.0f - momentum);
+    }
 }
 
 // SyncBN: the replicas' records [world][1 + 2C] = (count, mean[C], M2[C]) combined in rank order
@@ -395,6 +435,16 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
     const int s0 = blockIdx.y * kGroupSlabs, s1 = nch == 1 || s0 + kGroupSlabs > S ? S : s0 + kGroupSlabs;
     __shared__ double red[4][8][kLQ];
     __shared__ int flag;
+    // the writers' mean / rstd loaded up front: loaded after the first output store they would each
+    // wait for it (the pointers may alias), a chain of 8 round trips at the end of the launch
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < kLQ && c < C && use_bn) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mu[k] = mean[c + k];
+            rs[k] = rstd[c + k];
+        }
+    }
     double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     if (c < C) {
         int s = s0 + g;
@@ -463,9 +513,9 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
         const float s1v = (float)a[k], s2v = (float)a[4 + k];
         if (dbeta) dbeta[cc] = s1v;
         if (use_bn && dgamma) dgamma[cc] = s2v;
-        coef[cc] = use_bn ? mean[cc] : 0.f;
+        coef[cc] = use_bn ? mu[k] : 0.f;
         coef[C + cc] = use_bn ? s1v * invM : 0.f;
-        coef[2 * C + cc] = use_bn ? rstd[cc] * (s2v * invM) : 0.f;
+        coef[2 * C + cc] = use_bn ? rs[k] * (s2v * invM) : 0.f;
     }
 }
 
