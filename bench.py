@@ -89,7 +89,7 @@ def op_breakdown(summary):
     return rows
 
 
-def encoder_block_roofline(batch, size, device, reps=10, x3=True):
+def encoder_block_roofline(batch, size, device, reps=10, x3=True, fuse="auto"):
     """forward, training-mode conv blocks of the encoder (depthwise -> pointwise +
     BN-statistics epilogue; the BN apply + ReLU of the input is done on load, as in the train
     step) at `batch` images, each timed with HIP events around `reps` back-to-back launches (median
@@ -125,7 +125,7 @@ def encoder_block_roofline(batch, size, device, reps=10, x3=True):
             # the train step's own kernel choice (engine.block_fwd_choice): fused launch from the
             # 64 x 64 level up, y stored unless the block's weight gradients recompute it; split
             # depthwise + pointwise launches (y always stored) below
-            fused, keep_y = block_fwd_choice(view, batch, hh, hh, co, training=True)
+            fused, keep_y = block_fwd_choice(view, batch, hh, hh, co, training=True, fuse=fuse)
             pkx = None  # the split-precision weight planes the engine hands the fused kernel
             if fused and x3 and ck % 16 == 0 and ck >= 64:
                 pkx = torch.empty(3 * ck * co, dtype=torch.int16, device=device)
@@ -450,7 +450,8 @@ def main():
         if not args.no_roofline and world == 1 and args.encoder_batch > 0:
             del model
             torch.cuda.empty_cache()
-            out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device, x3=not args.no_x3)
+            out["encoder_blocks"] = encoder_block_roofline(args.encoder_batch, args.size, device, x3=not args.no_x3,
+                                                           fuse=args.fuse)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.size, args.num_classes, args.batch, args.cpu_warmup,
                                                args.cpu_steps, args.cpu_threads)

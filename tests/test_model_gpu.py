@@ -225,6 +225,39 @@ def test_inplace_weight_edit_reaches_split_planes():
     assert torch.equal(p1, p2)
 
 
+def test_large_batch_fuses_the_32x32_level():
+    """engine.block_fwd_choice fuses a level below 64 x 64 once the batch gives it >= 256 pixel
+    tiles (FUSE_MIN_TOTAL_PIXELS; the encoder table's batch 32 at the 32 x 32 level): on a 128 x 128
+    input the 32 x 32 blocks (enc3 / dec3) then run the fused bf16x6 forward with their split
+    planes (refreshed for that batch only), at batch 2 the split launches.  Against the all-split
+    route (fuse="never": fp32 GEMMs): the training loss to 1e-5 and the batch-32 prediction to
+    1e-5 relative L2.  (Gradients of this random-init net move by ~3e-3 between ANY two fp32
+    summation orders -- ReLU decisions flip -- as fp32 vs the float64 oracle does in the
+    train-geometry parity log; their parity is the op tests' and test_parity_sizes_gpu's.)"""
+    from unet_amd.model import UNetModel
+    rng = np.random.default_rng(23)
+    x, y = _data(rng, 32, 128, 128, 1)
+    xd = torch.from_numpy(x).cuda()
+    res = {}
+    for fuse in ("auto", "never"):
+        m = UNetModel((128, 128, 3), 1, dropout_rate=0.0, seed=9)
+        m.compile(None, "dice_loss")
+        m.engine.fuse_sepconv = fuse
+        p = m.engine.predict(xd).clone()
+        live = set(m.engine.x3_live)
+        loss = m.train_step(x, y)
+        torch.cuda.synchronize()
+        res[fuse] = (float(loss[0]), p)
+        if fuse == "auto":
+            assert {"enc3_block1", "enc3_block2", "dec3_block2"} <= live  # the 32 x 32 level at batch 32
+            assert "enc4_block1" not in live  # 16 x 16 at batch 32: 8192 pixels, split launches
+            m.engine.predict(xd[:2])
+            assert "enc3_block2" not in m.engine.x3_live and "enc2_block2" in m.engine.x3_live
+    (la, pa), (ln, pn) = res["auto"], res["never"]
+    assert abs(la - ln) <= 1e-5 * max(1.0, abs(ln))
+    assert float((pa - pn).double().norm() / pn.double().norm()) < 1e-5
+
+
 def test_stream_schedules_bitwise_equal():
     """The schedule only orders launches: single-stream, two-stream with the weight gradients issued
     beside their data gradient, and two-stream with the fused 256x256-level weight gradient deferred

@@ -35,6 +35,11 @@ DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
 
 
 FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools/bench_sepconv.py sweeps)
+# ... and on a smaller level once the batch gives it >= 256 pixel tiles: the 32 x 32 level at batch
+# 32 (the encoder table's batch, configs[4]'s whole batch): enc4 113.5 -> 84.9 / 225.4 -> 171.5 us
+# with its bf16x6 kernel; at batch 16 the split launches stay faster (10.59 vs 10.67 ms/step,
+# profiles/r5d_step_ab.txt fa_*)
+FUSE_MIN_TOTAL_PIXELS = 32 * 1024
 # blocks whose weight gradients recompute y instead of the forward storing it: an output channel count
 # (64: the fused block backward), or an (input, output) channel pair
 RECOMPUTE_Y_COUTS = (64,)
@@ -46,7 +51,7 @@ def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bo
     (else unet_dwconv3x3_fwd + unet_pointwise_fwd, which always store y); keep_y: the fused launch
     also stores the depthwise output y for the weight gradients (training blocks whose weight
     gradients do not recompute it).  Shared by the engine and bench.py's encoder table."""
-    want = fuse == "always" or (fuse == "auto" and h * w >= FUSE_MIN_PIXELS)
+    want = fuse == "always" or (fuse == "auto" and (h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS))
     if not (want and ops.sepconv_supported(view, n, h, w, cout)):
         return False, training
     y_recompute = training and recompute_y and (cout in recompute_couts or (view.channels, cout) in recompute_couts) and \
@@ -226,30 +231,40 @@ class UNetEngine:
 
     def _build_x3(self):
         """Split-precision planes (ops.split_x3) of the pointwise kernels of the blocks whose fused
-        forward can run the bf16x6 register-A kernel (>= 64 x 64 pixels, channels % 16 == 0):
-        one launch per weight update refreshes all of them."""
+        forward can run the bf16x6 register-A kernel (channels % 16 == 0, >= 64): one launch per
+        weight update refreshes the ones the forward's batch fuses (_refresh_x3)."""
         self.use_x3 = True
         self.x3_off: Dict[str, int] = {}
-        segs, off = [], 0
+        self.x3_cand = []  # (block, segment) in block order
+        off = 0
         for b in self.blocks:
-            h, w = self._dims(b.level)
-            if h * w >= FUSE_MIN_PIXELS and b.cin % 16 == 0 and b.cin >= 64 and not b.wcin:
+            if b.cin % 16 == 0 and b.cin >= 64 and not b.wcin:
                 src = self.train_layout.offsets[f"{b.name}_sepconv/pointwise_kernel"]
-                segs.append((src, b.cin, b.cout, off))
+                self.x3_cand.append((b, (src, b.cin, b.cout, off)))
                 self.x3_off[b.name] = off
                 off += (3 * b.cin * b.cout + 7) // 8 * 8
-        self.x3_segs = segs
+        self.x3_live: set = set()
         self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
 
-    def _refresh_x3(self):
+    def _refresh_x3(self, n: int):
         """Re-split on EVERY forward (one small launch): the planes then always match the fp32
         weights the backward reads, whatever wrote engine.params in between (AdamW, a custom
-        optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast)."""
-        if self.use_x3 and self.x3_segs:
-            ops.split_x3(self.params, self.x3_segs, self.pkx)
+        optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast).  Only the
+        blocks whose level the batch of n images fuses (block_fwd_choice's pixel rule)."""
+        self.x3_live = set()
+        if not self.use_x3:
+            return
+        segs = []
+        for b, seg in self.x3_cand:
+            h, w = self._dims(b.level)
+            if h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS:
+                segs.append(seg)
+                self.x3_live.add(b.name)
+        if segs:
+            ops.split_x3(self.params, segs, self.pkx)
 
     def _pkx(self, b: "Block"):
-        o = self.x3_off.get(b.name) if self.use_x3 else None
+        o = self.x3_off.get(b.name) if self.use_x3 and b.name in self.x3_live else None
         return None if o is None else self.pkx[o:o + 3 * b.cin * b.cout]
 
     def get_weights_dict(self) -> Dict[str, np.ndarray]:
@@ -461,7 +476,7 @@ class UNetEngine:
         if drop and seeds is None:
             seeds = self.drop_seeds(self.step_count + 1)
         x = self._padded_input(A, x)
-        self._refresh_x3()
+        self._refresh_x3(n)
         self._x_fwd = x
         v = View.plain(x)
         for stage, b1, b2 in self.enc:
