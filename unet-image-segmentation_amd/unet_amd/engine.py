@@ -244,6 +244,7 @@ class UNetEngine:
                 self.x3_off[b.name] = off
                 off += (3 * b.cin * b.cout + 7) // 8 * 8
         self.x3_live: set = set()
+        self._x3_plans: Dict[int, tuple] = {}
         self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
 
     def _refresh_x3(self, n: int):
@@ -251,15 +252,19 @@ class UNetEngine:
         weights the backward reads, whatever wrote engine.params in between (AdamW, a custom
         optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast).  Only the
         blocks whose level the batch of n images fuses (block_fwd_choice's pixel rule)."""
-        self.x3_live = set()
         if not self.use_x3:
+            self.x3_live = set()
             return
-        segs = []
-        for b, seg in self.x3_cand:
-            h, w = self._dims(b.level)
-            if h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS:
-                segs.append(seg)
-                self.x3_live.add(b.name)
+        plan = self._x3_plans.get(n)
+        if plan is None:  # (cached per batch size: the host loop is on the critical path of small steps)
+            segs, live = [], set()
+            for b, seg in self.x3_cand:
+                h, w = self._dims(b.level)
+                if h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS:
+                    segs.append(seg)
+                    live.add(b.name)
+            plan = self._x3_plans[n] = (segs, live)
+        segs, self.x3_live = plan
         if segs:
             ops.split_x3(self.params, segs, self.pkx)
 
