@@ -39,7 +39,7 @@ FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools
 # 32 (the encoder table's batch, configs[4]'s whole batch): enc4 113.5 -> 84.9 / 225.4 -> 171.5 us
 # with its bf16x6 kernel; at batch 16 the split launches stay faster (10.59 vs 10.67 ms/step,
 # profiles/r5d_step_ab.txt fa_*)
-FUSE_MIN_TOTAL_PIXELS = 32 * 1024
+FUSE_MIN_TOTAL_PIXELS = int(os.environ.get("UNET_FUSE_MIN_TOTAL", 32 * 1024))  # (env: A/B only)
 # blocks whose weight gradients recompute y instead of the forward storing it: an output channel count
 # (64: the fused block backward), or an (input, output) channel pair
 RECOMPUTE_Y_COUTS = (64,)
