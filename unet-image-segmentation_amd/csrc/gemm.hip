@@ -1371,8 +1371,10 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     const int env_bn = lab_knob("UNET_ROWS_BN", 0);
     if (env_bn > 0) return RowsCfg{env_bn, lab_knob("UNET_ROWS_BK", 16)};
     // grids of 128 x 128 tiles that leave CUs idle (the deep levels at small batch: 2048-8192
-    // rows) take 64-wide N tiles, twice the blocks
-    const bool narrow = lab_knob("UNET_ROWS_NARROW", 1) && a.N > 64 && cdiv(a.M, 128) * cdiv(a.N, 128) < 256;
+    // rows; up to one block per CU) take 64-wide N tiles, twice the blocks (<= 256 rather than
+    // < 256 blocks: -0.4 % per step at batch 16 and batch 8, profiles/r5d_step_ab.txt nw_*)
+    const bool narrow = lab_knob("UNET_ROWS_NARROW", 1) && a.N > 64 &&
+                        cdiv(a.M, 128) * cdiv(a.N, 128) < lab_knob("UNET_ROWS_NARROW_LT", 257);
     if (amode == A_BNBWD) {
         // lab: UNET_BNBWD_BK16 = 1 stages BK = 16 (40 KB of LDS instead of 72 KB at 128 columns:
         // co-residency with the side stream's weight-gradient blocks)
