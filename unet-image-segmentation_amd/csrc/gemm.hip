@@ -1389,8 +1389,11 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
     }
     const int bk32_k = lab_knob("UNET_BK32_MIN_K", 256);  // smallest K that takes BK = 32
     if (a.N <= 64) return RowsCfg{64, 16};
-    if (narrow) return RowsCfg{64, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
-    return RowsCfg{128, a.K >= bk32_k && amode != A_UNSHUFFLE ? 32 : 16};
+    // (the ConvT data gradient keeps BK = 16: BK = 32 runs its kernels 5-20 % faster alone but the
+    // step slower beside the side stream, profiles/r5d_step_ab.txt bk_*; lab UNET_UNSHUFFLE_BK32)
+    const bool bk32 = a.K >= bk32_k && (amode != A_UNSHUFFLE || lab_knob("UNET_UNSHUFFLE_BK32", 0));
+    if (narrow) return RowsCfg{64, bk32 ? 32 : 16};
+    return RowsCfg{128, bk32 ? 32 : 16};
 }
 
 template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false, int BM = 128>
@@ -1405,6 +1408,16 @@ void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
 // bound (MFMA pipe 27-54 % busy, PMC profiles/r3c_pmc_rows*.csv), so fewer MFMA cycles do not show.
 bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
 
+// Row-tile height of the ConvTranspose data gradient with BatchNorm partials (E_BNPART): 64
+// when the 128-row grid holds at most one block per CU (the bottleneck at batch 8: 16 x 16
+// blocks of 128 x 64) -- twice the blocks.  The partials are per row tile, so the slab count
+// (unet_conv_transpose2x2_bwd_data_bnstats_slabs) follows.  Lab: UNET_CONVT_BM64 = 0 off,
+// 2 takes 64 x 128 tiles (the same block count, half the N-tiles).
+int convt_bnpart_bm(int64_t M, int N) {
+    const int mode = lab_knob("UNET_CONVT_BM64", 1);
+    return mode && cdiv(M, 128) * cdiv(N, 64) <= 256 ? 64 : 128;
+}
+
 template <int AMODE, bool DROP, int EPI>
 int launch_rows(const RowsArgs& a0, hipStream_t st, const char* what) {
     RowsArgs a = a0;
@@ -1418,9 +1431,18 @@ int launch_rows(const RowsArgs& a0, hipStream_t st, const char* what) {
             return 0;
         }
 #endif
-        if constexpr (AMODE == A_BNBWD && EPI == E_STORE) {  // (the only 64-row tile: no per-128-row partials)
+        if constexpr (AMODE == A_BNBWD && EPI == E_STORE) {
             if (c.bm == 64) {
                 launch_rows_tile<128, 32, AMODE, DROP, EPI, false, 64>(a, st);
+                UNET_CHECK_LAUNCH(what);
+                return 0;
+            }
+        }
+        if constexpr (AMODE == A_UNSHUFFLE && EPI == E_BNPART) {
+            if (convt_bnpart_bm(a.M, (int)a.N) == 64) {
+                if (lab_knob("UNET_CONVT_BM64", 1) == 2) launch_rows_tile<128, 16, AMODE, DROP, EPI, false, 64>(a, st);
+                else if (c.bk == 32) launch_rows_tile<64, 32, AMODE, DROP, EPI, false, 64>(a, st);
+                else launch_rows_tile<64, 16, AMODE, DROP, EPI, false, 64>(a, st);
                 UNET_CHECK_LAUNCH(what);
                 return 0;
             }
@@ -1919,7 +1941,7 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats_slabs(const unet_view* x,
     if (x->c0 % 4 || cout % 4) return 0;
     const int64_t M = (int64_t)n * h * w;
     if (!fits_i32(M, x->c0) || !fits_i32(4 * M, cout)) return 0;
-    return (int)cdiv(M, 128);
+    return (int)cdiv(M, convt_bnpart_bm(M, x->c0));
 }
 
 extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h, int w, int cout,
