@@ -405,7 +405,7 @@ int qt_for(int C) {
 }
 
 struct TilePlan {
-    int qt, tw, tiles_w, tiles_h, chunks, ntiles;
+    int qt, tw, tiles_w, tiles_h, chunks, ntiles, n;
 };
 TilePlan tile_plan(int N, int H, int W, int C) {
     TilePlan p;
@@ -415,10 +415,14 @@ TilePlan tile_plan(int N, int H, int W, int C) {
     p.tiles_h = (int)cdiv(H, TH);
     p.chunks = p.qt ? C / (4 * p.qt) : 1;
     p.ntiles = N * p.tiles_w * p.tiles_h;
+    p.n = N;
     return p;
 }
 int filter_blocks(const TilePlan& p) {
-    int target = lab_knob("UNET_DWF_BLOCKS", 1024);  // persistent blocks over all channel chunks
+    // persistent blocks over all channel chunks: 1024 (~4 per CU), 512 at batch <= 8 (fewer slabs to
+    // reduce; configs[4] batch 8 -0.8 %, configs[3] and batch 16 / 32 within the spread or slower with
+    // 512, profiles/r5d_step_ab.txt d8_* / d16_* / dq_*)
+    int target = lab_knob("UNET_DWF_BLOCKS", p.n <= lab_knob("UNET_DWF_SMALL_N", 8) ? 512 : 1024);
     if (target < 1) target = 1024;
     int g = (int)cdiv(target, p.chunks);
     if (g > p.ntiles) g = p.ntiles;
