@@ -385,7 +385,9 @@ int unet_conv_transpose2x2_bwd(const unet_view* x, int n, int h, int w,
  * output feeding the upsample, u_net.py:88): dx is then the whole da of the
  * view's block, so the GEMM epilogue also emits that block's BatchNorm-backward
  * partials in the unet_dwconv3x3_bwd_data_bnstats format (S = _slabs(...)
- * slabs of 128 rows; mean/rstd NULL when use_batch_norm=False; finish with
+ * slabs, one per row tile: 128 rows, or 64 rows when the 128-row grid would
+ * hold <= 256 tiles of 64 columns (round 5); always size and finish with the
+ * S the query returns; mean/rstd NULL when use_batch_norm=False; finish with
  * unet_bn_relu_bwd_stats_finish).  Replaces unet_bn_relu_bwd_stats's separate
  * pass over (da, z).  A view with dropout (the bottleneck's, u_net.py:77-78;
  * round 5, no signature change): the partials are those of g = da * mask, as
