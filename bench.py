@@ -255,6 +255,50 @@ def cpu_baseline(size, ncls, batch, warmup=10, steps=10, threads=0):
                       f"max {r['max_step_s']})"}
 
 
+def dp_info_obj(backend, exposed_ms, bucketer, steps):
+    """The line's `data_parallel` object (world > 1): the backend, the all-reduce time the step
+    exposes on the main stream (measured by bench.py's probe pass), the bucket layout and the ring
+    volume per GPU, 2 (n - 1) / n x the gradient bytes."""
+    world = bucketer.world
+    grad_bytes = 4 * int(bucketer.grads.numel())
+    return {"backend": backend, "collective": "all_reduce(sum) of the flat fp32 gradient buffer, "
+            "bucketed, issued from the side stream as the backward completes each bucket",
+            "allreduce_exposed_ms": round(float(exposed_ms), 4),
+            "allreduce_exposed_definition": f"median over {steps} steps (max over ranks) of HIP-event time on "
+                                            "the main stream from the end of the backward to the last bucket",
+            "buckets": len(bucketer.buckets), "bucket_bytes": [4 * (hi - lo) for lo, hi in bucketer.buckets],
+            "grad_bytes": grad_bytes, "world": world,
+            "ring_bytes_per_gpu": round(2 * (world - 1) / world * grad_bytes)}
+
+
+def result_line(args, world, dt, loss):
+    """The JSON line's contract fields (rank 0): whole-job images/s over `world` ranks of
+    args.batch images each (weak scaling), the time of args.steps steps (max over ranks)."""
+    imgs = world * args.batch * args.steps
+    return {
+        "metric": "images/sec (train step, 256x256x3)",
+        "value": round(imgs / dt, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (x~U[0,1) NHWC, quad masks ~30% fg), random-init Keras-glorot weights",
+        "config": {"workload": f"{workload_config(args)}: {args.size}x{args.size}x3 "
+                               f"{'binary' if args.num_classes == 1 else f'{args.num_classes}-class'} U-Net train "
+                               f"step (fwd + dice_loss + bwd + AdamW + MeanIoU(2) update, dropout 0.2)",
+                   "network": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
+                   "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                   "seq_len": args.size * args.size, "parallelism": f"dp{world}",
+                   "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-replica"},
+        "final_loss": round(loss, 6),
+    }
+
+
 def spawn_ranks(n: int) -> int:
     """`bench.py --gpus N` without a launcher: run this same command as N torchrun ranks (one
     process per GPU) in a CHILD process and relay its exit code.  Called before anything touches
@@ -270,7 +314,7 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -298,9 +342,14 @@ def main():
                     help="data parallel: BatchNorm over the global batch (SyncBN) instead of per replica")
     ap.add_argument("--encoder-batch", type=int, default=32,
                     help="batch of the encoder-block roofline table (SURVEY 8(d)); 0 = skip")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    return args
+
+
+def main():
+    args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
@@ -402,40 +451,11 @@ def main():
         ex = sorted(a.elapsed_time(b) for a, b in probe)
         t = torch.tensor([ex[len(ex) // 2]], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        bk = model.bucketer
-        dp_info = {"backend": dist.get_backend(), "collective": "all_reduce(sum) of the flat fp32 gradient buffer, "
-                   "bucketed, issued from the side stream as the backward completes each bucket",
-                   "allreduce_exposed_ms": round(float(t.item()), 4),
-                   "allreduce_exposed_definition": f"median over {args.steps} steps (max over ranks) of HIP-event time on "
-                                                   "the main stream from the end of the backward to the last bucket",
-                   "buckets": len(bk.buckets), "bucket_bytes": [4 * (hi - lo) for lo, hi in bk.buckets],
-                   "grad_bytes": 4 * int(model.engine.grads.numel())}
+        dp_info = dp_info_obj(dist.get_backend(), float(t.item()), model.bucketer, args.steps)
 
     out = None
     if rank == 0:
-        imgs = world * args.batch * args.steps
-        out = {
-            "metric": "images/sec (train step, 256x256x3)",
-            "value": round(imgs / dt, 2),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (x~U[0,1) NHWC, quad masks ~30% fg), random-init Keras-glorot weights",
-            "config": {"workload": f"{workload_config(args)}: {args.size}x{args.size}x3 "
-                                   f"{'binary' if args.num_classes == 1 else f'{args.num_classes}-class'} U-Net train "
-                                   f"step (fwd + dice_loss + bwd + AdamW + MeanIoU(2) update, dropout 0.2)",
-                       "network": "U_NET separable-conv, filters 64-128-256-512, bneck 1024",
-                       "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                       "seq_len": args.size * args.size, "parallelism": f"dp{world}",
-                       "batchnorm": "sync" if (args.sync_bn and world > 1) else "per-replica"},
-            "final_loss": round(loss, 6),
-        }
+        out = result_line(args, world, dt, loss)
         if timer is not None:
             s = timer.summary().get(dominant)
             if s:

@@ -233,8 +233,32 @@ def class_masks(n, h, w, ncls, seed):
     return np.eye(ncls)[cls]
 
 
-def train_big_fixture(size, n, ncls, x_seed, w_seed):
-    """One train step (dropout 0) at a BASELINE training geometry, full widths, float64 oracle:
+DROP_SITES = ("bneck_dropout", "dec4_dropout", "dec3_dropout", "dec2_dropout")
+
+
+def _mix64(*vals):
+    """The engine's dropout-seed mixer (unet_amd/engine.py _mix64), restated so the fixture does not
+    need the device library: splitmix64 finalisers folded over the values."""
+    z = 0x243F6A8885A308D3
+    M = 0xFFFFFFFFFFFFFFFF
+    for v in vals:
+        z = (z ^ (int(v) & M)) & M
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+    return z
+
+
+def engine_drop_seeds(seed, step):
+    """Per-site dropout seeds of a single-process engine step (UNetEngine.drop_seeds, rank_salt 0):
+    the GPU test checks the engine still draws exactly these before comparing."""
+    return {s: _mix64(seed, step, i + 1) for i, s in enumerate(DROP_SITES)}
+
+
+def train_big_fixture(size, n, ncls, x_seed, w_seed, drop=0.0, engine_seed=2301):
+    """One train step at a BASELINE training geometry, full widths, float64 oracle (dropout off,
+    or `drop` = the reference's default 0.2 with the engine's first-step masks):
     loss, dice, every block's BatchNorm batch mean / variance, every gradient's norm, first 128
     values and a strided subsample (sub_index) with e32 = the same step in float32 (its own
     relative-L2 distance to float64 on that subsample, and over the whole tensor), and the first
@@ -243,9 +267,14 @@ def train_big_fixture(size, n, ncls, x_seed, w_seed):
     w = model_weights(ncls, FULL, w_seed)
     x = U(x_seed, (n, size, size, 3))
     y = quad_masks(n, size, size) if ncls == 1 else class_masks(n, size, size, ncls, x_seed + 1)
-    orc = UNetOracle(ncls, 0.0)
-    out = {"x_seed": x_seed, "w_seed": w_seed, "n": n, "size": size, "ncls": ncls}
-    prob, cache, stats = orc.forward(w, x, training=True)
+    orc = UNetOracle(ncls, drop)
+    seeds = engine_drop_seeds(engine_seed, 1) if drop > 0 else None
+    out = {"x_seed": x_seed, "w_seed": w_seed, "n": n, "size": size, "ncls": ncls, "drop": drop,
+           "engine_seed": engine_seed}
+    if seeds:
+        for k, v in seeds.items():
+            out["drop_seed:" + k] = np.uint64(v)
+    prob, cache, stats = orc.forward(w, x, training=True, drop_seeds=seeds)
     lval, dprob = orc.loss_and_dprob(y, prob)
     out["loss"], out["dice"] = lval, K.dice_coef(y, prob)
     for name, rec in cache.items():
@@ -267,7 +296,7 @@ def train_big_fixture(size, n, ncls, x_seed, w_seed):
             p1 = stats[k]
         out["new256:" + k] = p1.reshape(-1)[:256]
     w32 = {k: v.astype(np.float32) for k, v in w.items()}
-    prob32, cache32, _ = orc.forward(w32, x.astype(np.float32), training=True)
+    prob32, cache32, _ = orc.forward(w32, x.astype(np.float32), training=True, drop_seeds=seeds)
     _, dprob32 = orc.loss_and_dprob(y.astype(np.float32), prob32)
     del prob32
     g32, _ = orc.backward(w32, cache32, dprob32)
@@ -298,6 +327,20 @@ def train512_fixture():
     return train_big_fixture(512, 8, 1, 71, 13)
 
 
+def train256d_fixture():
+    """configs[1] as the reference trains and bench.py times it: 256x256x3 binary, batch 16, with
+    U_NET's default dropout_rate=0.2 (model/u_net.py:30, scripts/train.py:223) at the bottleneck and
+    dec4 / dec3 / dec2 (:77-78, 97-98); masks from the engine's step-1 seeds (engine_seed 2301)."""
+    return train_big_fixture(256, 16, 1, 81, 14, drop=0.2)
+
+
+def train256b32_fixture():
+    """configs[4] with its whole batch of 32 on one GPU (21 classes, 256x256x3, dropout 0.2): the batch
+    that routes the 32x32 level through the fused split-precision forward (engine FUSE_MIN_TOTAL_PIXELS;
+    the encoder table's batch, model/u_net.py:63-69)."""
+    return train_big_fixture(256, 32, 21, 91, 15, drop=0.2)
+
+
 def write(name, d):
     np.savez_compressed(os.path.join(HERE, name), **{k.replace("/", "|"): v for k, v in d.items()})
 
@@ -305,7 +348,8 @@ def write(name, d):
 BIG = {"fwd256.npz": fwd256_fixture, "fwd512.npz": fwd512_fixture, "fwd21.npz": fwd21_fixture,
        "samples.npz": samples_fixture, "train128.npz": train128_fixture, "train256.npz": train256_fixture,
        "train256c21.npz": train256c21_fixture,
-       "train512.npz": train512_fixture}
+       "train512.npz": train512_fixture, "train256d.npz": train256d_fixture,
+       "train256b32.npz": train256b32_fixture}
 
 
 if __name__ == "__main__" and len(sys.argv) > 1:  # regenerate only the named fixtures

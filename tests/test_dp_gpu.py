@@ -43,14 +43,17 @@ def test_dp_two_ranks_equal_weighted_single_process(global_batch, deferred):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("global_batch", [4, 5])
-def test_dp_sync_bn_equals_full_batch(global_batch):
+@pytest.mark.parametrize("global_batch,drop", [(4, False), (5, False), (5, True)])
+def test_dp_sync_bn_equals_full_batch(global_batch, drop):
     """tools/dp_syncbn_check.py: with SyncBN (model.enable_data_parallel(sync_bn=True), SURVEY 8(e)
     option) a two-rank step over shards 2+2 / 3+2 equals ONE single-process step over the whole
     global batch (dropout off): gradients within fp32 reduction order, moving statistics equal,
-    and every rank bitwise identical."""
+    and every rank bitwise identical.  drop: dropout 0.2 with SyncBN, against the same DP step
+    through the unfused BN-backward statistics route (the dropout-masked producer
+    partials feeding the SyncBN all-reduce)."""
     env = dict(os.environ)
     env["DP_CHECK_GLOBAL"] = str(global_batch)
+    env["DP_CHECK_DROP"] = "1" if drop else "0"
     if torch.cuda.device_count() < 2:
         env["UNET_DP_ONE_DEVICE"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

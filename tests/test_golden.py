@@ -40,7 +40,8 @@ def test_oracle_reproduces_train_golden():
         assert np.allclose(new[k], v, rtol=1e-9, atol=1e-15), k
 
 
-SLOW = ("train256.npz", "train256c21.npz", "train512.npz")  # 4-10 min of float64 oracle each: checked below
+SLOW = ("train256.npz", "train256c21.npz", "train512.npz", "train256d.npz",
+        "train256b32.npz")  # 4-20 min of float64 oracle each: checked below
 
 
 @pytest.mark.parametrize("name", sorted(set(MG.BIG) - set(SLOW)))
@@ -72,6 +73,9 @@ def test_training_geometry_goldens_consistent(name):
     assert {k[7:] for k in g if k.startswith("new256:")} == {s.name for s in specs}
     assert len([k for k in g if k.startswith("bn_mean:")]) == 18
     assert abs(float(g["dice"]) + float(g["loss"]) - 1.0) < 1e-12
+    if float(g.get("drop", 0.0)) > 0:  # the dropout masks are the engine's step-1 draws
+        seeds = MG.engine_drop_seeds(int(g["engine_seed"]), 1)
+        assert {k[10:]: int(v) for k, v in g.items() if k.startswith("drop_seed:")} == seeds
     w = MG.model_weights(ncls, MG.FULL, int(g["w_seed"]))
     for k in trainable:
         sub = g["gsub:" + k].astype(np.float64)

@@ -199,7 +199,8 @@ def test_train_step_128_batch4():
 
 @pytest.mark.parametrize("fixture,recompute128,x3", [("train256.npz", False, True), ("train256c21.npz", False, True),
                                                      ("train256.npz", True, True), ("train512.npz", False, True),
-                                                     ("train256c21.npz", False, False)])
+                                                     ("train256c21.npz", False, False), ("train256d.npz", False, True),
+                                                     ("train256b32.npz", False, True)])
 def test_train_step_training_geometry(fixture, recompute128, x3):
     """One train step at the geometry the reference trains at (scripts/train.py:84-88, 256x256)
     with configs[1]'s batch of 16 (binary) and configs[4]'s per-GPU batch of 8 (21 classes),
@@ -217,7 +218,14 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
     from unet_amd.optim import AdamW
     g = _load(fixture)
     size, n, ncls = int(g["size"]), int(g["n"]), int(g["ncls"])
-    m = UNetModel((size, size, 3), ncls, dropout_rate=0.0)
+    drop = float(g["drop"]) if "drop" in g else 0.0
+    # train256d / train256b32: the reference's default dropout_rate=0.2 (model/u_net.py:30,77-78,97-98;
+    # scripts/train.py:223), i.e. the step bench.py times, with the oracle's masks drawn from the
+    # engine's documented step-1 seeds (checked equal here before anything runs)
+    m = UNetModel((size, size, 3), ncls, dropout_rate=drop, seed=int(g["engine_seed"]) if drop else 2301)
+    if drop:
+        want = {k[10:]: int(v) for k, v in g.items() if k.startswith("drop_seed:")}
+        assert m.engine.drop_seeds(m.engine.step_count + 1) == want
     m.engine.use_x3 = x3  # False: the fp32-MFMA fused forward (the split-precision A/B)
     if recompute128:  # the 128-output blocks keep no y either: unet_sepconv_bwd_filter recomputes it
         m.engine.recompute_y_couts = (64, 128)
@@ -228,6 +236,9 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
     m.compile(AdamW(2e-3, 1e-4), "dice_loss")
     res = m.train_step(x.astype(np.float32), y.astype(np.float32)).cpu().numpy()
     torch.cuda.synchronize()
+    if n * (size // 8) ** 2 >= 32 * 1024 and x3:
+        # batch 32: the 32x32 level (enc4 / dec4) took the fused split-precision forward
+        assert {"enc4_block1", "enc4_block2", "dec4_block2"} <= m.engine.x3_live, m.engine.x3_live
     grads = {k: host(t) for k, t in m.engine.gvars.items()}
     neww = m.engine.get_weights_dict()
     # BatchNorm batch statistics of every block
@@ -270,7 +281,8 @@ def test_train_step_training_geometry(fixture, recompute128, x3):
         pre = bb.z.double() * bb.scale.double() + bb.shift.double()
         near0 += int((pre.abs() < 1e-6 * (bb.shift.double().abs().max() + 1)).sum())
     worst_cn = sorted(((k, *v) for k, v in cn_errs.items()), key=lambda r: -max(r[1], r[2]))[:5]
-    _log({"test": fixture, "x3": x3, "recompute128": recompute128, "worst_ratio_to_e32sub": worst_ratio,
+    _log({"test": fixture, "x3": x3, "recompute128": recompute128, "drop": drop, "fused32": sorted(m.engine.x3_live),
+          "worst_ratio_to_e32sub": worst_ratio,
           "loss": float(res[0]), "loss_ref": float(g["loss"]), "dice": float(res[1]),
           "bn_stats_worst_rel": bn_worst, "max_grad_rel_l2_sub": worst[0][1], "worst_grads": worst,
           "worst_channel_norms(name, last, second, e32 last, e32 second)": worst_cn,

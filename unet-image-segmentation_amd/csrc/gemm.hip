@@ -57,7 +57,8 @@ struct RowsArgs {
     const float* coef;  // A_BNBWD: (mu, p, q) x C
     float* side;        // A_BNBWD: optional copy of the formed A (= dz), written by N-tile 0
     const float *bsc, *bsh, *bmu, *brs;  // E_BNPART: per-column BN scale/shift, mean/rstd (NULL: no xhat)
-    float* bnpart;                       // E_BNPART: [cdiv(M, 128)][2][N] partial sums
+    float* bnpart;                       // E_BNPART: [cdiv(M, BM)][2][N] partial sums, one slab per row tile
+                                         //   (BM = 64 or 128, convt_bnpart_bm; sized by the _slabs query)
     float ep_rate, ep_inv_keep;          // E_BNPART: dropout between the block and C's consumer (rate 0: none);
     uint64_t ep_seed;                    //   g also carries the mask of element (m, n) (common.h drop_mult)
     int ko;  // lab build only (UNET_ROWS_KO): knock-out bits for timing decompositions, else 0

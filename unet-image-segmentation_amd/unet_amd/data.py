@@ -28,6 +28,14 @@ import numpy as np
 from .dp import shard_bounds
 
 
+def default_cache_cap() -> int:
+    """A quarter of the host's physical memory (the node-wide budget of the default decode caches)."""
+    try:
+        return os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE") // 4
+    except (ValueError, OSError, AttributeError):
+        return 64 << 30
+
+
 def local_world_size() -> int:
     """Data-parallel ranks on this host (torchrun's LOCAL_WORLD_SIZE; 1 without a launcher)."""
     try:
@@ -105,8 +113,9 @@ class PairLoader:
             host_gb = os.environ.get("UNET_LOADER_CACHE_HOST_GB")
             if host_gb:  # one host-wide budget over this node's ranks x (train + val) loaders
                 cache_bytes = int(float(host_gb) * (1 << 30)) // (2 * local_world_size())
-            else:
-                cache_bytes = 16 << 30
+            else:  # 16 GiB per loader, clamped so this node's ranks x (train + val) loaders stay
+                # within a quarter of physical memory (8 ranks x 2 loaders x 16 GiB)
+                cache_bytes = min(16 << 30, default_cache_cap() // (2 * local_world_size()))
         self.cache_bytes = int(cache_bytes)
         self._cache = {}
         self._cached_bytes = 0

@@ -39,19 +39,20 @@ FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools
 # 32 (the encoder table's batch, configs[4]'s whole batch): enc4 113.5 -> 84.9 / 225.4 -> 171.5 us
 # with its bf16x6 kernel; at batch 16 the split launches stay faster (10.59 vs 10.67 ms/step,
 # profiles/r5d_step_ab.txt fa_*)
-FUSE_MIN_TOTAL_PIXELS = int(os.environ.get("UNET_FUSE_MIN_TOTAL", 32 * 1024))  # (env: A/B only)
+# (fixed at import: every data-parallel rank takes the same route; an A/B sets engine.fuse_min_total)
+FUSE_MIN_TOTAL_PIXELS = 32 * 1024
 # blocks whose weight gradients recompute y instead of the forward storing it: an output channel count
 # (64: the fused block backward), or an (input, output) channel pair
 RECOMPUTE_Y_COUTS = (64,)
 
 
 def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bool, fuse: str = "auto",
-                     recompute_y: bool = True, recompute_couts=RECOMPUTE_Y_COUTS):
+                     recompute_y: bool = True, recompute_couts=RECOMPUTE_Y_COUTS, min_total: int = FUSE_MIN_TOTAL_PIXELS):
     """The kernels a conv_block forward runs: (fused, keep_y).  fused: one unet_sepconv_fwd launch
     (else unet_dwconv3x3_fwd + unet_pointwise_fwd, which always store y); keep_y: the fused launch
     also stores the depthwise output y for the weight gradients (training blocks whose weight
     gradients do not recompute it).  Shared by the engine and bench.py's encoder table."""
-    want = fuse == "always" or (fuse == "auto" and (h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS))
+    want = fuse == "always" or (fuse == "auto" and (h * w >= FUSE_MIN_PIXELS or n * h * w >= min_total))
     if not (want and ops.sepconv_supported(view, n, h, w, cout)):
         return False, training
     y_recompute = training and recompute_y and (cout in recompute_couts or (view.channels, cout) in recompute_couts) and \
@@ -176,6 +177,7 @@ class UNetEngine:
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
         # profiles/r1i_sepconv_bn_sweep.log); "always" / "never" force the choice (tests).
         self.fuse_sepconv = "auto"
+        self.fuse_min_total = FUSE_MIN_TOTAL_PIXELS  # ... and below 64 x 64 from this many pixels per launch
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
         # BN-backward statistics of a block emitted by the launch that completes its da (the next
@@ -255,15 +257,15 @@ class UNetEngine:
         if not self.use_x3:
             self.x3_live = set()
             return
-        plan = self._x3_plans.get(n)
+        plan = self._x3_plans.get((n, self.fuse_min_total))
         if plan is None:  # (cached per batch size: the host loop is on the critical path of small steps)
             segs, live = [], set()
             for b, seg in self.x3_cand:
                 h, w = self._dims(b.level)
-                if h * w >= FUSE_MIN_PIXELS or n * h * w >= FUSE_MIN_TOTAL_PIXELS:
+                if h * w >= FUSE_MIN_PIXELS or n * h * w >= self.fuse_min_total:
                     segs.append(seg)
                     live.add(b.name)
-            plan = self._x3_plans[n] = (segs, live)
+            plan = self._x3_plans[(n, self.fuse_min_total)] = (segs, live)
         segs, self.x3_live = plan
         if segs:
             ops.split_x3(self.params, segs, self.pkx)
@@ -362,7 +364,7 @@ class UNetEngine:
         gamma, beta, mm, mv = self._bn(b.name)
         dk, pk = self._wts(b)
         fused, keep_y = block_fwd_choice(view, n, h, w, b.cout, training, self.fuse_sepconv, self.recompute_y,
-                                         self.recompute_y_couts)
+                                         self.recompute_y_couts, self.fuse_min_total)
         if fused:
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view

@@ -75,7 +75,14 @@ class UNetModel:
     def enable_data_parallel(self, bucket_bytes: int = 6 << 20, group=None, sync_bn: bool = False):
         """Average gradients over torch.distributed ranks each step (bucketed, overlapped).
         sync_bn: BatchNorm over the global batch (SyncBN, SURVEY 8(e) option) instead of each
-        replica's shard (the reference's tf.distribute default, synchronized=False)."""
+        replica's shard (the reference's tf.distribute default, synchronized=False).
+
+        With sync_bn on, every training-mode forward (train_step, engine.forward(training=True),
+        model(x, training=True)) issues one blocking all-gather per BatchNorm and every backward
+        one all-reduce per BatchNorm, on the main stream: ALL ranks of the group must run them
+        together, in the same order, or the group hangs.  Inference (predict / evaluate,
+        training=False) uses the moving statistics and issues no collective, so it may run on
+        one rank alone."""
         import torch.distributed as dist
         self.bucketer = GradBucketer(self.engine.grads, bucket_bytes, group)
         self.engine.grad_hook = self.bucketer.ready
