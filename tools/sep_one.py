@@ -27,10 +27,13 @@ if opt == "x3":
 y = torch.empty(N, h, w, C, device="cuda")
 z = torch.empty(N, h, w, cout, device="cuda")
 part = torch.zeros(ops.bn_partials_numel(m, cout), device="cuda")
+# POOL=1: also the 2x2 max-pool selection epilogue (an encoder stage's block2, as the step runs it)
+zsel = torch.empty(N, h // 2, w // 2, cout, device="cuda") if os.environ.get("POOL") == "1" else None
+gam = torch.rand(cout, device="cuda") - 0.3 if zsel is not None else None
 for _ in range(iters):
     if opt == "split":
         ops.dwconv3x3_fwd(v, N, h, w, dk, y)
         ops.pointwise_fwd(y, m, C, cout, pk, z, part)
     else:
-        ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part, pkx=pkx)
+        ops.sepconv_fwd(v, N, h, w, dk, cout, pk, y, z, part, zsel, gam, pkx=pkx)
 torch.cuda.synchronize()
