@@ -54,14 +54,14 @@ struct PxLds {
 template <int MODE, bool DROP, bool STATS, int BN, int CIN, bool WRITE_Y, int PD>
 __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntiles) {
     static_assert(MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU || MODE == UNET_VIEW_CONCAT, "view");
-    static_assert(PD == 1 || PD == 2, "prefetch depth");
+    static_assert(PD >= 1 && PD <= 4, "prefetch depth");
     constexpr int TN = BN / 32;
     constexpr int NK = CIN / BK;
     constexpr int NH = PHPIX * (BK / 4);   // halo float4 per stage (720)
     constexpr int HR = (NH + 255) / 256;   // per thread (3)
     constexpr int BXN = 3 * BN * 2;        // 16-byte B chunks per stage
     constexpr int BXC = (BXN + 255) / 256;
-    constexpr int NSET = PD;               // register staging sets (st0, st1)
+    constexpr int NSET = PD;               // register staging sets (one per stage in flight)
     using L = PxLds<BN, CIN>;
     __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     float* const Xs0 = smem + L::X0;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
     // them in scratch memory, whose loads' vmcnt(0) waits drained the whole prefetch)
     float4 hx[NSET][HR];
     int hl[NSET][HR];  // linear pixel index of the element, -1 outside the image
-    uint4 rb0[BXC], rb1[BXC];
+    uint4 rb0[BXC], rb1[BXC], rb2[BXC], rb3[BXC];
     auto tile_geom = [&](int tile, int& n, int& h0, int& w0) {
         const int tw = tile % tiles_w, t2 = tile / tiles_w;
         w0 = tw * TW;
@@ -156,7 +156,9 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
             const bool ok = (BXN % 256 == 0) | (e < BXN);
             const uint4 v = *reinterpret_cast<const uint4*>(g.pkx + (ok ? ((int64_t)pl * g.Cout + nn) * CIN + k0 + 8 * c : 0));
             if constexpr (p == 0) rb0[j] = v;
-            else rb1[j] = v;
+            else if constexpr (p == 1) rb1[j] = v;
+            else if constexpr (p == 2) rb2[j] = v;
+            else rb3[j] = v;
         }
     };
     auto store = [&](int s, int slot, auto set) {
@@ -191,7 +193,9 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
             const int e = tid + 256 * j, pl = e / (2 * BN), rm = e - pl * 2 * BN, nn = rm >> 1, c = rm & 1;
             uint4 v;
             if constexpr (p == 0) v = rb0[j];
-            else v = rb1[j];
+            else if constexpr (p == 1) v = rb1[j];
+            else if constexpr (p == 2) v = rb2[j];
+            else v = rb3[j];
             if (BXN % 256 == 0 || e < BXN) *reinterpret_cast<uint4*>(Bb + (pl * BN + nn) * BK + 8 * (c ^ ((nn >> 3) & 1))) = v;
         }
     };
@@ -335,21 +339,26 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
     };
 
     // ---- the stage stream.  Slot s & 1 holds stage s; stage s + 1 was staged (registers -> LDS)
-    // at the end of stage s - 1.  PD = 2: register set (s + 1) & 1 holds stage s + 1 when stage s
-    // starts, set s & 1 holds stage s + 2 (both in flight); PD = 1: one set, stage s + 1.
+    // at the end of stage s - 1.  Register set t % PD holds stage t from its load until it is staged:
+    // when stage s starts, stages s + 1 ... s + PD are in flight (PD = 1: only s + 1).
     using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, NSET - 1>;
     if (S > 0) {
         load(0, S0{});
         store(0, 0, S0{});
-        if (S > 1) load(1, S1{});
-        if constexpr (PD == 2) {
-            if (S > 2) load(2, S0{});
+        if (S > 1) load(1, std::integral_constant<int, 1 % NSET>{});
+        if constexpr (PD >= 2) {
+            if (S > 2) load(2, std::integral_constant<int, 2 % NSET>{});
+        }
+        if constexpr (PD >= 3) {
+            if (S > 3) load(3, std::integral_constant<int, 3 % NSET>{});
+        }
+        if constexpr (PD >= 4) {
+            if (S > 4) load(4, std::integral_constant<int, 4 % NSET>{});
         }
     }
     __syncthreads();
     auto body = [&](int s, auto cur) {
-        // cur: the register set holding stage s + 1 (PD 2: (s + 1) & 1; PD 1: 0)
+        // cur: the register set holding stage s + 1, i.e. (s + 1) % PD
         compute(s, s & 1);
         if (s + 1 < S) {
             store(s + 1, (s + 1) & 1, cur);
@@ -360,9 +369,15 @@ __global__ __launch_bounds__(256, 2) void sepconv_px_kernel(SepArgs g, int ntile
         if (s % NK == NK - 1) epilogue(r + (s / NK) * G);
     };
     for (int s = 0; s < S; s += NSET) {
-        body(s, S1{});
-        if constexpr (PD == 2) {
-            if (s + 1 < S) body(s + 1, S0{});
+        body(s, std::integral_constant<int, 1 % NSET>{});
+        if constexpr (PD >= 2) {
+            if (s + 1 < S) body(s + 1, std::integral_constant<int, 2 % NSET>{});
+        }
+        if constexpr (PD >= 3) {
+            if (s + 2 < S) body(s + 2, std::integral_constant<int, 3 % NSET>{});
+        }
+        if constexpr (PD >= 4) {
+            if (s + 3 < S) body(s + 3, std::integral_constant<int, 4 % NSET>{});
         }
     }
     if constexpr (STATS) {
@@ -392,8 +407,10 @@ void launch_px_p(const SepArgs& a, bool stats, bool write_y, int ntiles, int gri
 
 template <int MODE, bool DROP>
 void launch_px_m(const SepArgs& a, bool stats, bool write_y, int pd, int ntiles, int grid, hipStream_t st) {
-#ifdef UNET_LAB_BUILD  // prefetch depth 1: lab only (UNET_PX_PD=1)
+#ifdef UNET_LAB_BUILD  // other prefetch depths: lab only (UNET_PX_PD=1, 3, 4)
     if (pd == 1) { launch_px_p<MODE, DROP, 1>(a, stats, write_y, ntiles, grid, st); return; }
+    if (pd == 3) { launch_px_p<MODE, DROP, 3>(a, stats, write_y, ntiles, grid, st); return; }
+    if (pd == 4) { launch_px_p<MODE, DROP, 4>(a, stats, write_y, ntiles, grid, st); return; }
 #endif
     (void)pd;
     launch_px_p<MODE, DROP, 2>(a, stats, write_y, ntiles, grid, st);

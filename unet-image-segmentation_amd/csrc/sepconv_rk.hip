@@ -38,7 +38,10 @@ template <int BN, bool X6 = false>
 struct RkLds {
     // X6: B as three bf16 planes [BN][16 k] (32-byte rows; the two 16-byte k chunks of row n are
     // swapped when bit 3 of n is set, so the fragment reads of 16-lane groups are conflict-free)
-    static constexpr int XSZ = HPIX * RX, KSZ = 9 * BK, BSZ = X6 ? 3 * BN * BK / 2 : BK * (BN + 4);
+    // X6: the stage's depthwise taps live in the halo pixels' pad floats (pixel i's 4 pad floats hold
+    // tap float4 i, i < 36), so a slot is 576 B smaller: at BN 128 three blocks fit a CU (3 x 53.76 KB;
+    // with a separate tap buffer the 54.78 KB allocation granule allowed two)
+    static constexpr int XSZ = HPIX * RX, KSZ = X6 ? 0 : 9 * BK, BSZ = X6 ? 3 * BN * BK / 2 : BK * (BN + 4);
     static constexpr int SLOTS = X6 ? 2 : 3;           // X6: two slots (53 KB: 3 blocks per CU; 79 KB at BN 256: 2)
     static constexpr int RING = SLOTS * (XSZ + KSZ + BSZ);
     static constexpr int EC = X6 && BN > 64 ? 64 : BN;  // accumulator columns per epilogue pass
@@ -167,7 +170,8 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
         }
         if (tid < 9 * (BK / 4)) {
             const int c2 = hc - 4 * hq + 4 * (tid % (BK / 4));
-            *reinterpret_cast<float4*>(&Ks(buf)[4 * tid]) = c2 < Cin ? htap : f4(0.f);
+            float* td = X6 ? &Xs(buf)[tid * RX + BK] : &Ks(buf)[4 * tid];  // X6: pixel tid's pad
+            *reinterpret_cast<float4*>(td) = c2 < Cin ? htap : f4(0.f);
         }
     };
     // ---- B staging: thread loads float4 (k-row, n-quad) of the n-contiguous weights
@@ -278,7 +282,6 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
         const int xoff8 = (pr * HWp + pc) * RX + 8 * hi;
         auto dw8 = [&](int b, float4& o0, float4& o1) {
             const float* X = Xs(b);
-            const float* Kt = Ks(b);
             o0 = f4(0.f);
             o1 = f4(0.f);
 #pragma unroll
@@ -286,9 +289,10 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
 #pragma unroll
                 for (int dx = 0; dx < 3; ++dx) {
                     const float* xp = &X[xoff8 + (dy * HWp + dx) * RX];
-                    const float* kp = &Kt[(dy * 3 + dx) * BK + 8 * hi];
+                    // tap float4 (dy * 3 + dx) * 4 + 2 hi (+ 1): the pads of those halo pixels
+                    const float* kp = &X[((dy * 3 + dx) * 4 + 2 * hi) * RX + BK];
                     o0 = fma4(*reinterpret_cast<const float4*>(xp), *reinterpret_cast<const float4*>(kp), o0);
-                    o1 = fma4(*reinterpret_cast<const float4*>(xp + 4), *reinterpret_cast<const float4*>(kp + 4), o1);
+                    o1 = fma4(*reinterpret_cast<const float4*>(xp + 4), *reinterpret_cast<const float4*>(kp + RX), o1);
                 }
         };
         float* yrow8 = nullptr;
