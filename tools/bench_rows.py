@@ -3,7 +3,7 @@ float64 product on the device, for the three rows-GEMM ops of the train step at 
 (batch 16, 256x256): the pointwise forward with the BN-statistics epilogue (split path levels),
 the BatchNorm-backward data gradient (the step's dominant op) and the Conv2DTranspose forward.
 
-    UNET_HIP_LIB=tools/lab/libunet_hip_lab.so UNET_X6=1 python tools/bench_rows.py TAG
+    UNET_HIP_LIB=tools/labbin/libunet_hip_lab.so UNET_X6=1 python tools/bench_rows.py TAG
 """
 import json
 import os

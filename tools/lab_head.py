@@ -2,7 +2,7 @@
 21 classes): forward, dice sums, fused backward, and the backward under knock-outs
 (UNET_HEAD_KO bits, lab library: 1 no loss_grad, 2 no input loads, 4 no dx stores, 8 no staging
 loads, 16 no db sums, 32 no phase-2 products, 64 no phase 1).
-usage: UNET_HIP_LIB=tools/lab/libunet_hip_lab.so python tools/lab_head.py KO [KO ...]"""
+usage: UNET_HIP_LIB=tools/labbin/libunet_hip_lab.so python tools/lab_head.py KO [KO ...]"""
 import json
 import os
 import subprocess

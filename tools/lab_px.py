@@ -3,7 +3,7 @@ one-tile-per-block register-A kernel (schedule RK1) on the short-K shapes (sched
 selection compared (bitwise expected: same products, same order) and the BN statistics partials
 (per tile, combined in a different order: ~1e-6 relative), and both timed with HIP events around
 back-to-back launches (median of 3 groups of 10).  With the lab library (UNET_HIP_LIB=
-tools/lab/libunet_hip_lab.so) UNET_PX_PD / UNET_PX_BPC select the prefetch depth / blocks per CU.
+tools/labbin/libunet_hip_lab.so) UNET_PX_PD / UNET_PX_BPC select the prefetch depth / blocks per CU.
 usage: python tools/lab_px.py [N] [check|time|both]"""
 import json
 import os
