@@ -1,4 +1,4 @@
-"""Data-parallel plumbing on CPU with the gloo backend (world size 2 and 4): the same
+"""Data-parallel plumbing on CPU with the gloo backend (world size 2, 4 and 8): the same
 GradBucketer the GPU path uses (RCCL there) averages a flat gradient buffer exactly, with
 buckets launched as the backward's low-water mark passes them; sharding of a global batch;
 and DP with the oracle as each rank's compute equals the single-process average."""
@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])  # 8: the driver's scaling node, rehearsed on CPU
 def test_bucketed_allreduce_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
