@@ -50,6 +50,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// pointer types __builtin_amdgcn_global_load_lds takes (global source, LDS destination)
+typedef __attribute__((address_space(1))) const void gbl_void;
+typedef __attribute__((address_space(3))) void lds_void;
+
 // ------------------------------------------------ fp32 as three bf16 (split-precision GEMMs) ----
 // x == hi + mid + lo EXACTLY for every finite normal fp32 x: hi = RNE_bf16(x), mid = RNE_bf16(x - hi),
 // lo = x - hi - mid (both differences are exact in fp32 and lo has at most 8 significant bits).

@@ -64,8 +64,7 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
     constexpr int NP = MODE == UNET_VIEW_POOL_BNRELU ? 4 : 1;
     constexpr int BQ = X6 ? 1 : BN * (BK / 4) / 256;  // B float4 per thread per stage
     constexpr int LB = BN + 4;                  // k-major B row stride
-    constexpr int BXN = 3 * BN * 2;             // X6: 16-byte B chunks per stage
-    constexpr int BXC = X6 ? (BXN + 255) / 256 : 1;
+    constexpr int BXN = 3 * BN * 2;             // X6: 16-byte B chunks per stage (a multiple of 64)
     using L = RkLds<BN, X6>;
     __shared__ __attribute__((aligned(16))) float smem[L::SIZE];
     auto Xs = [&](int b) { return smem + b * L::XSZ; };
@@ -192,28 +191,38 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
         for (int r = 0; r < BQ; ++r)
             *reinterpret_cast<float4*>(&Bs(buf)[(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = bok[r] ? rb[r] : f4(0.f);
     };
-    // X6 B staging: 16-byte chunks (plane, column, k half) of the pre-split planes, clamped loads
-    uint4 rbx[BXC];
-    bool bxok[BXC];
-    auto load_bx = [&](int k0) {
+    // X6 B staging by LDS-DMA (global_load_lds_dwordx4, no VGPR destination): LDS chunk q = 64 i + lane
+    // of a slot is (row q >> 1 = plane * BN + column, k half (q & 1) ^ bit 3 of the column) -- the
+    // image is lane-linear, so the conflict-free swizzle goes on the source address.  Wave w issues
+    // wave-instructions i = w, w + 4, ... of the stage's BXN / 64.  Columns past Cout load column 0
+    // (finite data; their accumulators are never stored); k always lies inside Cin (Cin % 16 == 0).
+    // Issued from inline asm: hipcc's wait bookkeeping would put vmcnt(0) before every ds_read while
+    // a DMA it knows of is in flight; the kernel waits for it itself (dma_wait).
+    constexpr int NIW = (BXN / 64 + 3) / 4;     // DMA wave-instructions per wave and stage
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    int bxo[X6 ? NIW : 1];
 #pragma unroll
-        for (int j = 0; j < BXC; ++j) {
-            const int e = tid + 256 * j, pl = e / (2 * BN), r = e - pl * 2 * BN, nn = r >> 1, c = r & 1;
-            bxok[j] = e < BXN && n0 + nn < g.Cout && k0 + 8 * c < Cin;
-            rbx[j] = *reinterpret_cast<const uint4*>(
-                g.pkx + (bxok[j] ? ((int64_t)pl * g.Cout + n0 + nn) * Cin + k0 + 8 * c : 0));
+    for (int j = 0; j < (X6 ? NIW : 1); ++j) {
+        const int q = (wv + 4 * j) * 64 + lane, row = q >> 1, pl = row / BN, nn = row - pl * BN;
+        const int c = (q & 1) ^ ((nn >> 3) & 1), col = n0 + nn < g.Cout ? n0 + nn : 0;
+        bxo[j] = (pl * g.Cout + col) * Cin + 8 * c;
+    }
+    auto dma_bx = [&](int k0, int buf) {
+        const unsigned base = (unsigned)(uintptr_t)(lds_void*)Bs(buf);
+#pragma unroll
+        for (int j = 0; j < NIW; ++j) {
+            const int i = wv + 4 * j;
+            if ((BXN / 64) % 4 == 0 || i < BXN / 64) {
+                const unsigned short* src = g.pkx + bxo[j] + k0;
+                const unsigned dst = base + i * 1024;
+                unsigned keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+            }
         }
     };
-    auto store_bx = [&](int buf) {
-        unsigned short* Bb = reinterpret_cast<unsigned short*>(Bs(buf));
-#pragma unroll
-        for (int j = 0; j < BXC; ++j) {
-            const int e = tid + 256 * j, pl = e / (2 * BN), r = e - pl * 2 * BN, nn = r >> 1, c = r & 1;
-            if (e < BXN)
-                *reinterpret_cast<uint4*>(Bb + (pl * BN + nn) * BK + 8 * (c ^ ((nn >> 3) & 1))) =
-                    bxok[j] ? rbx[j] : make_uint4(0u, 0u, 0u, 0u);
-        }
-    };
+    // every vector-memory operation of this wave retired (the DMA, and the stage's y stores)
+    auto dma_wait = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
     // ---- this lane's pixel: tile row 2 wave + (lo >> 4), column rk_col(lo)
     const int pr = 2 * wave + (lo >> 4), pc = rk_col(lo);
@@ -301,17 +310,19 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
         // they are written to the other slot after the compute, then stage kt + 2's are issued.
         // Only stage 0's loads are exposed (one latency per block, not two: at 4-8 stages per
         // block that is most of the prologue)
+        // B: stage kt + 1's planes are DMA'd into the other slot at the top of stage kt (free since
+        // the barrier that ended stage kt - 1: its lgkmcnt(0) retired the slot's fragment reads);
+        // dma_wait after store_halo -- before stage kt + 2's halo loads are issued -- retires them
+        // ahead of the stage's barrier, the only thing that orders them for the next stage's reads
         load_halo(0);
-        load_bx(0);
+        dma_bx(0, 0);
         store_halo(0);
-        store_bx(0);
-        if (nk > 1) {
-            load_halo(BK);
-            load_bx(BK);
-        }
+        dma_wait();
+        if (nk > 1) load_halo(BK);
         __syncthreads();
         for (int kt = 0; kt < nk; ++kt) {
             const int cb = kt & 1, wb = cb ^ 1;
+            if (kt + 1 < nk) dma_bx((kt + 1) * BK, wb);
             // this stage's depthwise (VALU), then its MFMAs: with two waves per SIMD one wave's
             // depthwise runs beside the other's MFMAs (a look-ahead inside the wave needed ~60 more
             // registers and spilled)
@@ -344,11 +355,8 @@ __global__ __launch_bounds__(256, X6 && BN <= 128 ? 3 : 2) void sepconv_rk_kerne
             }
             if (kt + 1 < nk) {
                 store_halo(wb);
-                store_bx(wb);
-                if (kt + 2 < nk) {
-                    load_halo((kt + 2) * BK);
-                    load_bx((kt + 2) * BK);
-                }
+                dma_wait();
+                if (kt + 2 < nk) load_halo((kt + 2) * BK);
             }
             __syncthreads();
         }
