@@ -226,8 +226,8 @@ def test_inplace_weight_edit_reaches_split_planes():
 
 
 def test_large_batch_fuses_the_32x32_level():
-    """engine.block_fwd_choice fuses a level below 64 x 64 once the batch gives it >= 256 pixel
-    tiles (FUSE_MIN_TOTAL_PIXELS; the encoder table's batch 32 at the 32 x 32 level): on a 128 x 128
+    """engine.block_fwd_choice fuses a level below 64 x 64 once the batch gives it >= 128 pixel
+    tiles (FUSE_MIN_TOTAL_PIXELS: the 32 x 32 level from batch 16): on a 128 x 128
     input the 32 x 32 blocks (enc3 / dec3) then run the fused bf16x6 forward with their split
     planes (refreshed for that batch only), at batch 2 the split launches.  Against the all-split
     route (fuse="never": fp32 GEMMs): the training loss to 1e-5 and the batch-32 prediction to
