@@ -329,6 +329,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-x3", action="store_true",
                     help="fp32-MFMA fused forward instead of its split-precision (bf16x6) variant (A/B)")
+    ap.add_argument("--no-x6-gemm", action="store_true",
+                    help="fp32-MFMA rows GEMMs (BN-backward data gradient, ConvT forward / data gradient, split-"
+                         "route pointwise forward) instead of their split-precision (bf16x6) route (A/B)")
     ap.add_argument("--no-fused-bwd", action="store_true",
                     help="64-output blocks: data-gradient GEMM + side-stream weight-gradient pass instead of "
                          "the fused block backward (A/B)")
@@ -376,6 +379,7 @@ def main():
     if world > 1:
         model.enable_data_parallel(sync_bn=args.sync_bn)
     model.engine.use_x3 = not args.no_x3
+    model.engine.x6_gemm = not args.no_x6_gemm
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
     if args.recompute_y128:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 11
+#define UNET_ABI_VERSION 12
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -94,6 +94,11 @@ int unet_copy_strided(const float* src, int64_t rows, int cols, int64_t src_ld, 
 #define UNET_SPLIT_MAX_SEGS 32
 int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
                   unet_stream_t stream);
+/* The same split with the planes in the source layout, [3][rows][cols] (ABI 12): the operand
+ * layout of the split-precision data-gradient GEMM (unet_pointwise_bwd_data_bnrelu_x3 reads
+ * pw_kernel (Cin, Cout) with k = Cout contiguous).                                            */
+int unet_split_x3_keep(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                       unet_stream_t stream);
 
 /* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
  * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers
@@ -149,6 +154,11 @@ size_t unet_bn_partials_size(int64_t m, int c); /* bytes of bn_partials */
 int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout,
                        const float* pw_kernel, float* z, float* bn_partials,
                        unet_stream_t stream);
+/* The same with pw_kernel_x3 = unet_split_x3(pw_kernel) ([3][Cout][Cin], unet_sepconv_fwd's planes;
+ * ABI 12): the bf16x6 split-precision GEMM of unet_pointwise_bwd_data_bnrelu_x3 where cin % 32 == 0. */
+int unet_pointwise_fwd_x3(const float* y, int64_t m, int cin, int cout, const float* pw_kernel,
+                          const unsigned short* pw_kernel_x3, float* z, float* bn_partials,
+                          unet_stream_t stream);
 /* dy[m, ci] = sum_co dz[m, co] * k[ci, co] */
 int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout,
                             const float* pw_kernel, float* dy,
@@ -326,6 +336,19 @@ int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m,
                                    const float* coef, float drop_rate,
                                    uint64_t drop_seed, float* dy, float* dz,
                                    unet_stream_t stream);
+/* The same with pw_kernel_x3 = unet_split_x3_keep(pw_kernel) ([3][Cin][Cout] bf16 planes, 16-B
+ * aligned; ABI 12): where cout % 32 == 0 the GEMM runs the six significant bf16 part products
+ * of both operands on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the A operand, dz, is
+ * split exactly as it is formed), the split-precision form of unet_sepconv_fwd's pw_kernel_x3:
+ * fp32-accurate (relative error ~2^-23 per product), not bitwise equal to the fp32-MFMA route.
+ * pw_kernel is still read where the route does not apply.                                   */
+int unet_pointwise_bwd_data_bnrelu_x3(const float* da, const float* z, int64_t m,
+                                      int cin, int cout, const float* pw_kernel,
+                                      const unsigned short* pw_kernel_x3,
+                                      const float* scale, const float* shift,
+                                      const float* coef, float drop_rate,
+                                      uint64_t drop_seed, float* dy, float* dz,
+                                      unet_stream_t stream);
 
 /* The image block (enc1_block1 over the 3-channel input zero-padded to 4):
  * unet_pointwise_bwd_data_bnrelu without dropout, cin == 4, cout 32 or 64,
@@ -371,6 +394,11 @@ int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w,
                                int cout, const float* kernel,
                                const float* bias, float* out,
                                unet_stream_t stream);
+/* The same with kernel_x3 = unet_split_x3_keep(kernel as (4 cout, cin)) (ABI 12): the bf16x6
+ * split-precision GEMM of unet_pointwise_bwd_data_bnrelu_x3 where cin % 32 == 0.            */
+int unet_conv_transpose2x2_fwd_x3(const unet_view* x, int n, int h, int w, int cout,
+                                  const float* kernel, const unsigned short* kernel_x3,
+                                  const float* bias, float* out, unet_stream_t stream);
 size_t unet_conv_transpose2x2_bwd_workspace(int n, int h, int w, int cin,
                                             int cout);
 /* dx (n,h,w,Cin) = grad w.r.t. the view output (NULL: skip); dkernel, dbias
@@ -404,6 +432,13 @@ int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h,
                                             const float* rstd,
                                             float* bn_partials,
                                             unet_stream_t stream);
+/* The same with kernel_x3t = unet_split_x3(kernel as (4 cout, cin)) ([3][cin][4 cout] planes,
+ * ABI 12): the bf16x6 GEMM where cout % 8 == 0 and the partials are per 128-row tile.      */
+int unet_conv_transpose2x2_bwd_data_bnstats_x3(const unet_view* x, int n, int h, int w, int cout,
+                                               const float* kernel, const unsigned short* kernel_x3t,
+                                               const float* dout, float* dx, const float* mean,
+                                               const float* rstd, float* bn_partials,
+                                               unet_stream_t stream);
 
 /* ----- Output layer Conv2D(ncls, 1, activation) — u_net.py:105-112 --------
  * prob = sigmoid(x.k + b) (ncls == 1) or softmax over channels.            */

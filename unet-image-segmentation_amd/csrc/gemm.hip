@@ -62,6 +62,7 @@ struct RowsArgs {
     float ep_rate, ep_inv_keep;          // E_BNPART: dropout between the block and C's consumer (rate 0: none);
     uint64_t ep_seed;                    //   g also carries the mask of element (m, n) (common.h drop_mult)
     int ko;  // lab build only (UNET_ROWS_KO): knock-out bits for timing decompositions, else 0
+    const unsigned short* Bx;  // split-precision route: B as three bf16 planes [3][N][K] (k contiguous), or NULL
 };
 #ifdef UNET_LAB_BUILD
 #define ROWS_KO(g, bit) (((g).ko & (bit)) != 0)
@@ -329,6 +330,7 @@ struct WgradArgs {
     const float* bz;     // W_BNBWD: raw z (same layout as b.src0)
     const float* bcoef;  // W_BNBWD: (mu, p, q) x Q
     float* colpart;      // optional [S][P]: column sums of A over the block's m slice (vectorised kernel, q-tile 0)
+    bool x6;             // 128 x 128 tiles take the split-precision (bf16x6) kernel
 };
 
 template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP>
@@ -470,11 +472,17 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(WgradArgs g) {
 // k0+s and k-slot 1 = k0+4+s, so lane (row, half) feeds 4 consecutive MFMAs from ONE
 // ds_read_b128 of its row.  Row stride BK+4 floats makes those reads conflict-free.
 //
-// X6 (split precision, see common.h split4 / mfma_x6): the staged A and B values are split into
-// three bf16 planes each as they are written to LDS ([row][k] images, k contiguous, row stride
-// BK + 8 bf16 = conflict-free ds_read_b128), and every 16-deep k step runs the six
+// X6 (split precision, see common.h split4 / mfma_x6): the staged A values are split into three
+// bf16 planes as they are written to LDS ([row][k] images, k contiguous, row stride BK + 8 bf16 =
+// conflict-free ds_read_b128); B arrives pre-split (g.Bx, [3][N][K] planes written once per weight
+// update by unet_split_x3_ex) and is copied 16 bytes at a time.  Every 16-deep k step runs the six
 // v_mfma_f32_32x32x16_bf16 of mfma_x6 per 32x32 tile: 6 x 32 cycles instead of the 8 x 64 of
-// v_mfma_f32_32x32x2_f32, at fp32 accuracy.  Loads, operand views and epilogues are shared.
+// v_mfma_f32_32x32x2_f32, at fp32 accuracy.  The bf16 MFMA leaves 24 of its 32 issue cycles to
+// VALU (the f32 MFMA shares the FP32 vector datapath), so the BN-backward operand transform and
+// the split hide under the matrix work.  With 2.7x fewer matrix cycles per stage the load latency
+// is what a stage must cover: X6 stages BK = 32 in ONE LDS buffer (61 KB at 128 x 128: two blocks
+// per CU), loads of stage k+1 in registers while stage k computes, two barriers per stage (the
+// co-resident block's MFMAs fill the store phase).  Loads, operand views and epilogues are shared.
 #ifdef UNET_LAB_BUILD
 // lab: ko bits 8-15 = stagger (that many s_sleep 32, ~2048 cycles each) for the second half of the
 // grid's blocks (bit 16: the odd blocks instead), so the two blocks sharing a CU do not run in lockstep
@@ -505,7 +513,7 @@ __device__ unsigned long long lab_rows_stamps[65536 * 4];
 #endif
 
 template <int BM, int BN, int BK, int AMODE, bool DROP, int EPI, bool BKC, bool X6 = false>
-__global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
+__global__ __launch_bounds__(256, X6 ? 2 : 1) void gemm_rows_vec(RowsArgs g) {
     main_stream_prio();
     ROWS_STAGGER(g);
     ROWS_STAMP(g, 0);
@@ -519,14 +527,23 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     constexpr int TM = BM / 64, TN = BN / 64;
     constexpr int BSZ = BKC ? BN * LR : BK * LB;
     constexpr int F32_BYTES = 4 * 2 * (BM * LR + BSZ);
-    constexpr int X6_BYTES = 2 * 2 * 3 * (BM + BN) * XR;
+    // X6 + BatchNorm backward: the five per-channel operand vectors (scale, shift, mu, p, q) of all
+    // K <= X6_KMAX channels sit in LDS (read per stage), not in 20 live registers across the k-loop
+    constexpr int X6_KMAX = 512;
+    constexpr bool XCOEF = X6 && AMODE == A_BNBWD;
+    constexpr int X6_BYTES = 2 * 3 * (BM + BN) * XR + (XCOEF ? 4 * 5 * X6_KMAX : 0);  // one buffer
+    static_assert(!X6 || BK == 32, "X6 rows GEMM: 32-deep stages");
     __shared__ __attribute__((aligned(16))) char smem[X6 ? X6_BYTES : F32_BYTES];
+    float* xcoef = reinterpret_cast<float*>(smem + 2 * 3 * (BM + BN) * XR);  // XCOEF: [5][X6_KMAX]
     // fp32 images (the X6 path uses the first bytes of As as epilogue scratch only)
     float (*As)[BM * LR] = reinterpret_cast<float (*)[BM * LR]>(smem);
     float (*Bs)[BSZ] = reinterpret_cast<float (*)[BSZ]>(smem + 4 * 2 * BM * LR);
-    // X6 planes: Ax[(buf * 3 + plane) * BM + row][k], Bx[(buf * 3 + plane) * BN + col][k]
+    // X6 planes: Ax[plane * BM + row][k], Bx[plane * BN + col][k]
     unsigned short* Ax = reinterpret_cast<unsigned short*>(smem);
-    unsigned short* Bx = Ax + 2 * 3 * BM * XR;
+    unsigned short* Bx = Ax + 3 * BM * XR;
+    // X6: B chunks (8 bf16 of one plane row) per thread and stage
+    constexpr int XCH = BK / 8, XQ = 3 * BN * XCH / 256;
+    static_assert(!X6 || (3 * BN * XCH) % 256 == 0, "X6: whole B chunks per thread");
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -581,6 +598,21 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
     float4 csc, csh, cmu, cp, cq;  // per-stage channel constants of this thread's k-quad
     int ak = 0;                    // k of this thread's A quad in the staged k-stage
     bool bok[BQ];
+    uint4 rx[X6 ? XQ : 1];        // X6: staged B plane chunks
+    bool xok[X6 ? XQ : 1];
+    int xoff[X6 ? XQ : 1], xlds[X6 ? XQ : 1];  // chunk's plane-row element offset at k0 = 0 (-1: out of range) / LDS slot
+    if constexpr (X6) {
+        const int64_t plane = (int64_t)g.N * K;
+#pragma unroll
+        for (int j = 0; j < XQ; ++j) {
+            const int c = tid + 256 * j;
+            const int p = c / (BN * XCH), rem = c - p * (BN * XCH);
+            const int row = rem / XCH, kc = rem - row * XCH;
+            const int n = n0 + row;
+            xoff[j] = n < g.N ? (int)(p * plane + (int64_t)n * K) + 8 * kc : -1;
+            xlds[j] = (p * BN + row) * XR + 8 * kc;
+        }
+    }
     auto load_stage = [&](int k0) {
         const int k = k0 + 4 * kq;
         ak = k;
@@ -592,11 +624,11 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             const int co = kc - ab * g.uf;
             koff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
         }
-        if constexpr (AMODE == A_BNRELU || AMODE == A_BNBWD) {
+        if constexpr ((AMODE == A_BNRELU || AMODE == A_BNBWD) && !XCOEF) {
             csc = ld4(g.a.sc0 + kc);
             csh = ld4(g.a.sh0 + kc);
         }
-        if constexpr (AMODE == A_BNBWD) {
+        if constexpr (AMODE == A_BNBWD && !XCOEF) {
             cmu = ld4(g.coef + kc);
             cp = ld4(g.coef + K + kc);
             cq = ld4(g.coef + 2 * K + kc);
@@ -607,15 +639,30 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             ra[r] = ld4(g.a.src0 + o);
             if constexpr (AMODE == A_BNBWD) rz[r] = ld4(g.z + o);
         }
+        if constexpr (X6) {
+#pragma unroll
+            for (int j = 0; j < XQ; ++j) {  // (K % BK == 0 on this route: every chunk's k exists)
+                xok[j] = xoff[j] >= 0;
+                rx[j] = *reinterpret_cast<const uint4*>(g.Bx + (xok[j] ? xoff[j] + k0 : 0));
+            }
+        } else {
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const int kk = BKC ? k0 + 4 * bq_k : k0 + bq_k + (256 / NQ) * r;
             bok[r] = boff[r] >= 0 && kk < K;
             rb[r] = ld4(g.B + (bok[r] ? boff[r] + (BKC ? k0 : k0 * sbk) : 0));
         }
+        }
     };
     auto store_stage = [&](int buf) {
         const bool kv = ak < K;
+        if constexpr (XCOEF) {  // (ak < K on this route: K % 32 == 0)
+            csc = *reinterpret_cast<const float4*>(xcoef + ak);
+            csh = *reinterpret_cast<const float4*>(xcoef + X6_KMAX + ak);
+            cmu = *reinterpret_cast<const float4*>(xcoef + 2 * X6_KMAX + ak);
+            cp = *reinterpret_cast<const float4*>(xcoef + 3 * X6_KMAX + ak);
+            cq = *reinterpret_cast<const float4*>(xcoef + 4 * X6_KMAX + ak);
+        }
 #pragma unroll
         for (int r = 0; r < AQ; ++r) {
             float4 v = ra[r];
@@ -642,7 +689,7 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             const int row = arow + (256 / KQ) * r;
             if constexpr (X6) {
                 const Split4 sp = split4(v);
-                unsigned short* d = Ax + (buf * 3 * BM + row) * XR + 4 * kq;
+                unsigned short* d = Ax + row * XR + 4 * kq;
                 *reinterpret_cast<uint2*>(d) = sp.h;
                 *reinterpret_cast<uint2*>(d + BM * XR) = sp.m;
                 *reinterpret_cast<uint2*>(d + 2 * BM * XR) = sp.l;
@@ -650,29 +697,16 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
                 *reinterpret_cast<float4*>(&As[buf][row * LR + 4 * kq]) = v;
             }
         }
+        if constexpr (X6) {
+#pragma unroll
+            for (int j = 0; j < XQ; ++j)
+                *reinterpret_cast<uint4*>(Bx + xlds[j]) = xok[j] ? rx[j] : make_uint4(0u, 0u, 0u, 0u);
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < BQ; ++r) {
             const float4 v = bok[r] ? rb[r] : f4(0.f);
-            if constexpr (X6) {
-                const Split4 sp = split4(v);
-                if constexpr (BKC) {  // 4 consecutive k of one column
-                    unsigned short* d = Bx + (buf * 3 * BN + bq_n + (256 / KQ) * r) * XR + 4 * bq_k;
-                    *reinterpret_cast<uint2*>(d) = sp.h;
-                    *reinterpret_cast<uint2*>(d + BN * XR) = sp.m;
-                    *reinterpret_cast<uint2*>(d + 2 * BN * XR) = sp.l;
-                } else {  // 4 consecutive columns of one k: transposed into the [col][k] image
-                    unsigned short* d = Bx + (buf * 3 * BN + 4 * bq_n) * XR + bq_k + (256 / NQ) * r;
-                    const unsigned hw[4] = {sp.h.x & 0xFFFFu, sp.h.x >> 16, sp.h.y & 0xFFFFu, sp.h.y >> 16};
-                    const unsigned mw[4] = {sp.m.x & 0xFFFFu, sp.m.x >> 16, sp.m.y & 0xFFFFu, sp.m.y >> 16};
-                    const unsigned lw[4] = {sp.l.x & 0xFFFFu, sp.l.x >> 16, sp.l.y & 0xFFFFu, sp.l.y >> 16};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        d[j * XR] = (unsigned short)hw[j];
-                        d[BN * XR + j * XR] = (unsigned short)mw[j];
-                        d[2 * BN * XR + j * XR] = (unsigned short)lw[j];
-                    }
-                }
-            } else if constexpr (BKC) {
+            if constexpr (BKC) {
                 *reinterpret_cast<float4*>(&Bs[buf][(bq_n + (256 / KQ) * r) * LR + 4 * bq_k]) = v;
             } else {
                 *reinterpret_cast<float4*>(&Bs[buf][(bq_k + (256 / NQ) * r) * LB + 4 * bq_n]) = v;
@@ -689,7 +723,17 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
             for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
     const int nk = (K + BK - 1) / BK;
+    if constexpr (XCOEF) {
+        for (int i = tid; i < K; i += 256) {
+            xcoef[i] = g.a.sc0[i];
+            xcoef[X6_KMAX + i] = g.a.sh0[i];
+            xcoef[2 * X6_KMAX + i] = g.coef[i];
+            xcoef[3 * X6_KMAX + i] = g.coef[K + i];
+            xcoef[4 * X6_KMAX + i] = g.coef[2 * K + i];
+        }
+    }
     load_stage(0);
+    if constexpr (XCOEF) __syncthreads();
     store_stage(0);
     __syncthreads();
     ROWS_STAMP(g, 1);
@@ -699,23 +743,33 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
         if constexpr (X6) {
 #pragma unroll
             for (int ks = 0; ks < BK / 16; ++ks) {
-                bf16x8 af[TM][3], bfr[TN][3];
+                // the wave's B fragments for this 16-deep step, then one row tile's A fragments at a
+                // time (36 operand registers instead of 48)
+                bf16x8 bfr[TN][3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-#pragma unroll
-                    for (int tm = 0; tm < TM; ++tm)
-                        af[tm][p] = *reinterpret_cast<const bf16x8*>(
-                            Ax + ((buf * 3 + p) * BM + wm * (BM / 2) + tm * 32 + lo) * XR + ks * 16 + 8 * hi);
+                for (int p = 0; p < 3; ++p)
 #pragma unroll
                     for (int tn = 0; tn < TN; ++tn)
                         bfr[tn][p] = *reinterpret_cast<const bf16x8*>(
-                            Bx + ((buf * 3 + p) * BN + wn * (BN / 2) + tn * 32 + lo) * XR + ks * 16 + 8 * hi);
+                            Bx + (p * BN + wn * (BN / 2) + tn * 32 + lo) * XR + ks * 16 + 8 * hi);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    bf16x8 af[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        af[p] = *reinterpret_cast<const bf16x8*>(
+                            Ax + (p * BM + wm * (BM / 2) + tm * 32 + lo) * XR + ks * 16 + 8 * hi);
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af, bfr[tn], acc[tm][tn]);
                 }
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af[tm], bfr[tn], acc[tm][tn]);
             }
+            // one buffer: every wave's fragment reads are done before the next stage overwrites it
+            __syncthreads();
+            if (kt + 1 < nk) {
+                store_stage(0);
+                __syncthreads();
+            }
+            continue;
         } else {
 #pragma unroll
         for (int kg = 0; kg < BK / 8; ++kg) {
@@ -908,27 +962,29 @@ __global__ __launch_bounds__(256) void gemm_rows_vec(RowsArgs g) {
 
 // ------------------------------------------------------------- vectorised wgrad GEMM ----
 // X6 (split precision, 128 x 128 tiles): the reduction runs over pixels m, which both operands
-// hold m-major, so the bf16 planes are written transposed, [channel][m] with a 40-byte row (16 m +
-// 4 pad): threads 0-127 stage A, 128-255 B, each 4 consecutive m of one channel quad (lane
-// (quad, m-quad) = (u / 4, u % 4)): after an in-register 4 x 4 transpose every channel's 4 m go out
-// as one 8-byte store per plane, conflict-free at that row stride, and the MFMA fragments (8 m of
-// a channel) come back as two conflict-free ds_read_b64 (the 40-byte rows are not 16-byte aligned).
+// hold m-major, so the bf16 planes are written transposed, [channel][m] with an 80-byte row (32 m +
+// 8 pad, conflict-free ds_read_b128 fragments): threads 0-127 stage A, 128-255 B (whole waves), each
+// two groups of 4 consecutive m of one channel quad (lane (quad, m-octet) = (u / 4, u % 4)): after an
+// in-register 4 x 4 transpose every channel's 4 m go out as one 8-byte store per plane.  As in the
+// rows GEMM's X6 route the stages are 32 m deep in ONE LDS buffer (two blocks per CU, two barriers
+// per stage), so a stage's matrix work covers the next stage's load latency.
 template <int BP, int BQ, int AMODE, bool ADROP, int BMODE, bool BDROP, bool X6 = false>
-__global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
+__global__ __launch_bounds__(256, X6 ? 2 : 1) void gemm_wgrad_vec(WgradArgs g) {
     static_assert(!X6 || (BP == 128 && BQ == 128), "X6 wgrad: 128 x 128 tiles");
+    constexpr int KB = X6 ? 32 : BK;                 // m per stage
     constexpr int LDA = BP + 4, LDB = BQ + 4;
     constexpr int TM = BP / 64, TN = BQ / 64;
     constexpr int PQ = BP / 4, QQ = BQ / 4;          // quads per m-row
-    constexpr int AR = X6 ? 4 : BK * PQ / 256, BR = X6 ? 4 : BK * QQ / 256;
+    constexpr int AR = X6 ? 8 : BK * PQ / 256, BR = X6 ? 8 : BK * QQ / 256;
     constexpr int AS = X6 ? 1 : 256 / PQ, BS = X6 ? 1 : 256 / QQ;  // m-row step between a thread's quads
-    constexpr int XW = 20;                           // X6 plane row stride (bf16): 16 m + 4 pad
+    constexpr int XW = KB + 8;                       // X6 plane row stride (bf16): 32 m + 8 pad
     constexpr int F32_BYTES = 4 * 2 * BK * (LDA + LDB);
-    constexpr int X6_BYTES = 2 * 2 * 3 * (BP + BQ) * XW;
+    constexpr int X6_BYTES = 2 * 3 * (BP + BQ) * XW;  // one buffer
     __shared__ __attribute__((aligned(16))) char smem[X6 ? X6_BYTES : F32_BYTES];
     float (*As)[BK * LDA] = reinterpret_cast<float (*)[BK * LDA]>(smem);
     float (*Bs)[BK * LDB] = reinterpret_cast<float (*)[BK * LDB]>(smem + 4 * 2 * BK * LDA);
-    unsigned short* Ax = reinterpret_cast<unsigned short*>(smem);  // [(buf * 3 + plane) * BP + p][m]
-    unsigned short* Bx = Ax + 2 * 3 * BP * XW;                     // [(buf * 3 + plane) * BQ + q][m]
+    unsigned short* Ax = reinterpret_cast<unsigned short*>(smem);  // [plane * BP + p][m]
+    unsigned short* Bx = Ax + 3 * BP * XW;                         // [plane * BQ + q][m]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wp = wave >> 1, wq = wave & 1;
@@ -943,7 +999,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     const bool roleA = !X6 || tid < 128, roleB = !X6 || tid >= 128;
     const int unit = tid & 127;
 
-    const int apq = X6 ? unit >> 2 : tid % PQ, amm = X6 ? 4 * (unit & 3) : tid / PQ;
+    const int apq = X6 ? unit >> 2 : tid % PQ, amm = X6 ? 8 * (unit & 3) : tid / PQ;
     const int p = p0 + 4 * apq;
     const bool pv = p < g.P;
     float4 asc = f4(1.f), ash = f4(0.f);
@@ -959,7 +1015,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         const int co = p - ab * g.uf;
         poff = (ab >> 1) * (2 * g.uW * g.uf) + (ab & 1) * g.uf + co;
     }
-    const int bqq = X6 ? unit >> 2 : tid % QQ, bmm = X6 ? 4 * (unit & 3) : tid / QQ;
+    const int bqq = X6 ? unit >> 2 : tid % QQ, bmm = X6 ? 8 * (unit & 3) : tid / QQ;
     const int q = q0 + 4 * bqq;
     const bool qv = q < g.Q;
     float4 bsc = f4(1.f), bsh = f4(0.f), bmu = f4(0.f), bp_ = f4(0.f), bq_ = f4(0.f);
@@ -1037,7 +1093,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         if constexpr (AMODE == W_UNSHUFFLE) {
 #pragma unroll
             for (int r = 0; r < AR; ++r) {
-                uj[r] += BK;
+                uj[r] += KB;
                 while (uj[r] >= g.uW) {
                     uj[r] -= g.uW;
                     ++ur[r];
@@ -1064,8 +1120,13 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     };
     auto store_stage = [&](int buf) {
         if constexpr (X6) {
-            if (roleA) store_t4(Ax + (buf * 3 * BP + 4 * apq) * XW + amm, BP, ra);
-            else store_t4(Bx + (buf * 3 * BQ + 4 * bqq) * XW + bmm, BQ, rb);
+            if (roleA) {
+                store_t4(Ax + 4 * apq * XW + amm, BP, ra);
+                store_t4(Ax + 4 * apq * XW + amm + 4, BP, ra + 4);
+            } else {
+                store_t4(Bx + 4 * bqq * XW + bmm, BQ, rb);
+                store_t4(Bx + 4 * bqq * XW + bmm + 4, BQ, rb + 4);
+            }
         } else {
 #pragma unroll
             for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[buf][(amm + AS * r) * LDA + 4 * apq]) = ra[r];
@@ -1086,7 +1147,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
-    const int nk = (me - mb + BK - 1) / BK;
+    const int nk = (me - mb + KB - 1) / KB;
     if (nk > 0) {
         load_stage(mb);
         store_stage(0);
@@ -1094,30 +1155,34 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) load_stage(mb + (kt + 1) * BK);
+        if (kt + 1 < nk) load_stage(mb + (kt + 1) * KB);
         if constexpr (X6) {
-            bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
+            for (int ks = 0; ks < KB / 16; ++ks) {
+                bf16x8 bfr[TN][3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        bfr[tn][pl] = *reinterpret_cast<const bf16x8*>(
+                            Bx + (pl * BQ + wq * (BQ / 2) + tn * 32 + lo) * XW + ks * 16 + 8 * hi);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm) {
-                    const unsigned short* a =
-                        Ax + ((buf * 3 + pl) * BP + wp * (BP / 2) + tm * 32 + lo) * XW + 8 * hi;
-                    const uint2 u0 = *reinterpret_cast<const uint2*>(a), u1 = *reinterpret_cast<const uint2*>(a + 4);
-                    af[tm][pl] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
-                }
+                    bf16x8 af[3];
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn) {
-                    const unsigned short* b =
-                        Bx + ((buf * 3 + pl) * BQ + wq * (BQ / 2) + tn * 32 + lo) * XW + 8 * hi;
-                    const uint2 u0 = *reinterpret_cast<const uint2*>(b), u1 = *reinterpret_cast<const uint2*>(b + 4);
-                    bfr[tn][pl] = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+                    for (int pl = 0; pl < 3; ++pl)
+                        af[pl] = *reinterpret_cast<const bf16x8*>(
+                            Ax + (pl * BP + wp * (BP / 2) + tm * 32 + lo) * XW + ks * 16 + 8 * hi);
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af, bfr[tn], acc[tm][tn]);
                 }
             }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mfma_x6(af[tm], bfr[tn], acc[tm][tn]);
+            __syncthreads();  // one buffer: every wave's fragment reads done before it is rewritten
+            if (kt + 1 < nk) {
+                store_stage(0);
+                __syncthreads();
+            }
+            continue;
         } else {
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
@@ -1140,7 +1205,7 @@ __global__ __launch_bounds__(256) void gemm_wgrad_vec(WgradArgs g) {
         float4* T = reinterpret_cast<float4*>(&As[0][0]);
         T[tid] = csum;
         __syncthreads();
-        if constexpr (X6) {  // thread u < 128 holds quad u / 4, m-quad u % 4
+        if constexpr (X6) {  // thread u < 128 holds quad u / 4, m-octet u % 4
             if (tid < PQ && p0 + 4 * tid < g.P) {
                 float4 t = T[4 * tid];
                 for (int j = 1; j < 4; ++j) t = add4(t, T[4 * tid + j]);
@@ -1400,14 +1465,20 @@ RowsCfg rows_cfg(const RowsArgs& a, int amode) {
 template <int BN, int BKk, int AMODE, bool DROP, int EPI, bool X6 = false, int BM = 128>
 void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
     dim3 grid((unsigned)cdiv(a.M, BM), (unsigned)cdiv(a.N, BN));
-    if (a.sbk == 1) gemm_rows_vec<BM, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
+    if (X6 || a.sbk == 1) gemm_rows_vec<BM, BN, BKk, AMODE, DROP, EPI, true, X6><<<grid, 256, 0, st>>>(a);
     else gemm_rows_vec<BM, BN, BKk, AMODE, DROP, EPI, false, X6><<<grid, 256, 0, st>>>(a);
 }
 
-// Split-precision (bf16x6) rows / wgrad GEMMs: lab build only (UNET_X6).  Measured (tools/bench_rows.py,
-// profiles/r3_x6_rows_ab.jsonl): no faster than fp32 MFMA here -- these GEMMs are load-latency
-// bound (MFMA pipe 27-54 % busy, PMC profiles/r3c_pmc_rows*.csv), so fewer MFMA cycles do not show.
-bool rows_x6() { return lab_knob("UNET_X6", 0) != 0; }
+// Split-precision (bf16x6) rows GEMM: taken when the caller hands pre-split B planes (a.Bx) and
+// the k-loop is whole 32-deep stages.  (Round 3's form -- B split in every block, 16-deep stages in
+// a double buffer at one block per CU -- was load-latency bound and no faster than fp32 MFMA,
+// profiles/r3_x6_rows_ab.jsonl; lab UNET_X6 = 0 turns the route off for A/B runs.)
+// Grids of fewer than 256 128 x 128 tiles keep the fp32 route, whose narrow tiles fill the chip (the
+// bottleneck's data gradient at batch 16, 32 x 4 tiles: 61 vs 77 us, profiles/r6x_rows_x6.txt).
+bool rows_x6(const RowsArgs& a, int amode) {
+    return a.Bx != nullptr && a.K % 32 == 0 && (amode != A_BNBWD || a.K <= 512) &&
+           cdiv(a.M, 128) * cdiv(a.N, 128) >= lab_knob("UNET_X6_MIN_TILES", 256) && lab_knob("UNET_X6", 1) != 0;
+}
 
 // Row-tile height of the ConvTranspose data gradient with BatchNorm partials (E_BNPART): 64
 // when the 128-row grid holds at most one block per CU (the bottleneck at batch 8: 16 x 16
@@ -1425,13 +1496,11 @@ int launch_rows(const RowsArgs& a0, hipStream_t st, const char* what) {
     a.ko = lab_knob("UNET_ROWS_KO", 0);  // 1 no C stores, 2 no dz side copy, 4 no k-loop loads (lab)
     if (rows_vec_ok(a, AMODE)) {
         const RowsCfg c = rows_cfg(a, AMODE);
-#ifdef UNET_LAB_BUILD  // (not compiled into the product library)
-        if (rows_x6()) {
-            launch_rows_tile<128, 16, AMODE, DROP, EPI, true>(a, st);
+        if (rows_x6(a, AMODE)) {
+            launch_rows_tile<128, 32, AMODE, DROP, EPI, true>(a, st);
             UNET_CHECK_LAUNCH(what);
             return 0;
         }
-#endif
         if constexpr (AMODE == A_BNBWD && EPI == E_STORE) {
             if (c.bm == 64) {
                 launch_rows_tile<128, 32, AMODE, DROP, EPI, false, 64>(a, st);
@@ -1493,7 +1562,8 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     return w;
 }
 
-bool wgrad_x6() { return lab_knob("UNET_X6", 0) != 0; }
+// Split-precision weight gradients (both operands split as they are staged): 128 x 128 tiles.
+bool wgrad_x6() { return lab_knob("UNET_WGRAD_X6", 0) != 0; }
 
 template <int AMODE, bool ADROP, int BMODE, bool BDROP>
 void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
@@ -1503,12 +1573,10 @@ void launch_wgrad_t(const WgradArgs& a, const WgradPlan& w, hipStream_t st) {
                      (AMODE == W_UNSHUFFLE || a.a.c0 % 4 == 0) && a.b.c0 % 4 == 0 &&
                      ((uintptr_t)a.a.src0 | (uintptr_t)a.b.src0) % 16 == 0;
     if (vec || BMODE == W_BNBWD) {
-#ifdef UNET_LAB_BUILD
-        if (w.bp == 128 && w.bq == 128 && wgrad_x6()) {
+        if (w.bp == 128 && w.bq == 128 && a.x6 && wgrad_x6()) {
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP, true><<<grid, 256, pad, st>>>(a);
             return;
         }
-#endif
         if (w.bp == 128 && w.bq == 128)
             gemm_wgrad_vec<128, 128, AMODE, ADROP, BMODE, BDROP><<<grid, 256, pad, st>>>(a);
         else if (w.bp == 128)
@@ -1538,6 +1606,7 @@ int run_wgrad(WgradArgs a, int amode, int bmode, float* out, void* ws, size_t ws
     UNET_CHECK_ARG(ws && ws_bytes >= need, "%s: workspace %zu < %zu", what, ws_bytes, need);
     a.mslice = w.mslice;
     a.slab = static_cast<float*>(ws);
+    a.x6 = true;
     const bool ad = a.a.rate > 0.f, bd = a.b.rate > 0.f;
     if (amode == W_PLAIN && bmode == W_PLAIN) {
         launch_wgrad_t<W_PLAIN, false, W_PLAIN, false>(a, w, st);
@@ -1589,8 +1658,9 @@ extern "C" size_t unet_bn_partials_size(int64_t m, int c) {
     return bn_partials_bytes(m, c);  // partials + the finalize's chunk scratch (bn.hip)
 }
 
-extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, const float* pw_kernel, float* z,
-                                  float* bn_partials, unet_stream_t stream) {
+namespace {
+int pw_fwd(const float* y, int64_t m, int cin, int cout, const float* pw_kernel, const unsigned short* pw_kernel_x3,
+           float* z, float* bn_partials, unet_stream_t stream) {
     UNET_CHECK_ARG(y && pw_kernel && z, "unet_pointwise_fwd: null pointer");
     UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_fwd: bad sizes");
     UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_fwd: tensor too large");
@@ -1599,6 +1669,7 @@ extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, 
     a.M = m;
     a.K = cin;
     a.B = pw_kernel;
+    a.Bx = pw_kernel_x3;  // [3][cout][cin]: k = ci contiguous
     a.sbk = cout;
     a.sbn = 1;
     a.N = cout;
@@ -1608,6 +1679,19 @@ extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, 
     hipStream_t st = as_stream(stream);
     if (bn_partials) return launch_rows<A_PLAIN, false, E_STATS>(a, st, "unet_pointwise_fwd");
     return launch_rows<A_PLAIN, false, E_STORE>(a, st, "unet_pointwise_fwd");
+}
+}  // namespace
+
+extern "C" int unet_pointwise_fwd(const float* y, int64_t m, int cin, int cout, const float* pw_kernel, float* z,
+                                  float* bn_partials, unet_stream_t stream) {
+    return pw_fwd(y, m, cin, cout, pw_kernel, nullptr, z, bn_partials, stream);
+}
+extern "C" int unet_pointwise_fwd_x3(const float* y, int64_t m, int cin, int cout, const float* pw_kernel,
+                                     const unsigned short* pw_kernel_x3, float* z, float* bn_partials,
+                                     unet_stream_t stream) {
+    UNET_CHECK_ARG(pw_kernel_x3 && (uintptr_t)pw_kernel_x3 % 16 == 0,
+                   "unet_pointwise_fwd_x3: pw_kernel_x3 must be a 16-B aligned plane set");
+    return pw_fwd(y, m, cin, cout, pw_kernel, pw_kernel_x3, z, bn_partials, stream);
 }
 
 extern "C" int unet_pointwise_bwd_data(const float* dz, int64_t m, int cin, int cout, const float* pw_kernel,
@@ -1659,10 +1743,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dz_kernel(const float* __restrict_
 }
 }  // namespace
 
-extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout,
-                                              const float* pw_kernel, const float* scale, const float* shift,
-                                              const float* coef, float drop_rate, uint64_t drop_seed, float* dy,
-                                              float* dz, unet_stream_t stream) {
+namespace {
+int pw_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout, const float* pw_kernel,
+                       const unsigned short* pw_kernel_x3, const float* scale, const float* shift, const float* coef,
+                       float drop_rate, uint64_t drop_seed, float* dy, float* dz, unet_stream_t stream) {
     UNET_CHECK_ARG(da && z && pw_kernel && scale && shift && coef && dy, "unet_pointwise_bwd_data_bnrelu: null pointer");
     UNET_CHECK_ARG(m > 0 && cin > 0 && cout > 0, "unet_pointwise_bwd_data_bnrelu: bad sizes");
     UNET_CHECK_ARG(fits_i32(m, cin) && fits_i32(m, cout), "unet_pointwise_bwd_data_bnrelu: tensor too large");
@@ -1682,6 +1766,7 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
     a.M = m;
     a.K = cout;
     a.B = pw_kernel;  // B(k = co, n = ci) = k[ci][co]
+    a.Bx = pw_kernel_x3;
     a.sbk = 1;
     a.sbn = cout;
     a.N = cin;
@@ -1707,6 +1792,7 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
         p.M = m;
         p.K = cout;
         p.B = pw_kernel;
+        p.Bx = pw_kernel_x3;
         p.sbk = 1;
         p.sbn = cout;
         p.N = cin;
@@ -1717,6 +1803,26 @@ extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, i
     if (drop_rate > 0.f)
         return launch_rows<A_BNBWD, true, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
     return launch_rows<A_BNBWD, false, E_STORE>(a, st, "unet_pointwise_bwd_data_bnrelu");
+}
+}  // namespace
+
+extern "C" int unet_pointwise_bwd_data_bnrelu(const float* da, const float* z, int64_t m, int cin, int cout,
+                                              const float* pw_kernel, const float* scale, const float* shift,
+                                              const float* coef, float drop_rate, uint64_t drop_seed, float* dy,
+                                              float* dz, unet_stream_t stream) {
+    return pw_bwd_data_bnrelu(da, z, m, cin, cout, pw_kernel, nullptr, scale, shift, coef, drop_rate, drop_seed, dy,
+                              dz, stream);
+}
+
+extern "C" int unet_pointwise_bwd_data_bnrelu_x3(const float* da, const float* z, int64_t m, int cin, int cout,
+                                                 const float* pw_kernel, const unsigned short* pw_kernel_x3,
+                                                 const float* scale, const float* shift, const float* coef,
+                                                 float drop_rate, uint64_t drop_seed, float* dy, float* dz,
+                                                 unet_stream_t stream) {
+    UNET_CHECK_ARG(pw_kernel_x3 && (uintptr_t)pw_kernel_x3 % 16 == 0,
+                   "unet_pointwise_bwd_data_bnrelu_x3: pw_kernel_x3 must be a 16-B aligned plane set");
+    return pw_bwd_data_bnrelu(da, z, m, cin, cout, pw_kernel, pw_kernel_x3, scale, shift, coef, drop_rate, drop_seed,
+                              dy, dz, stream);
 }
 
 namespace {
@@ -1829,8 +1935,9 @@ extern "C" int unet_pointwise_bwd_filter(const float* y, const float* dz, int64_
 }
 
 // ------------------------------------------------------------ transposed conv 2x2/2 ----
-extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
-                                          const float* bias, float* out, unet_stream_t stream) {
+namespace {
+int convt_fwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel, const unsigned short* kernel_x3,
+              const float* bias, float* out, unet_stream_t stream) {
     if (check_view(x, "unet_conv_transpose2x2_fwd")) return -1;
     UNET_CHECK_ARG(x->mode == UNET_VIEW_PLAIN || x->mode == UNET_VIEW_BNRELU,
                    "unet_conv_transpose2x2_fwd: input view must be PLAIN or BNRELU");
@@ -1843,6 +1950,7 @@ extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int 
     a.M = M;
     a.K = cin;
     a.B = kernel;  // B(k = ci, n = (a, b, co)) = k[(a*2+b)*cout + co][ci]
+    a.Bx = kernel_x3;
     a.sbk = 1;
     a.sbn = cin;
     a.N = 4 * cout;
@@ -1859,6 +1967,19 @@ extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int 
     }
     if (drop) return launch_rows<A_BNRELU, true, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
     return launch_rows<A_BNRELU, false, E_SHUFFLE>(a, st, "unet_conv_transpose2x2_fwd");
+}
+}  // namespace
+
+extern "C" int unet_conv_transpose2x2_fwd(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
+                                          const float* bias, float* out, unet_stream_t stream) {
+    return convt_fwd(x, n, h, w, cout, kernel, nullptr, bias, out, stream);
+}
+extern "C" int unet_conv_transpose2x2_fwd_x3(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
+                                             const unsigned short* kernel_x3, const float* bias, float* out,
+                                             unet_stream_t stream) {
+    UNET_CHECK_ARG(kernel_x3 && (uintptr_t)kernel_x3 % 16 == 0,
+                   "unet_conv_transpose2x2_fwd_x3: kernel_x3 must be a 16-B aligned plane set");
+    return convt_fwd(x, n, h, w, cout, kernel, kernel_x3, bias, out, stream);
 }
 
 namespace {
@@ -1945,10 +2066,10 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats_slabs(const unet_view* x,
     return (int)cdiv(M, convt_bnpart_bm(M, x->c0));
 }
 
-extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h, int w, int cout,
-                                                       const float* kernel, const float* dout, float* dx,
-                                                       const float* mean, const float* rstd, float* bn_partials,
-                                                       unet_stream_t stream) {
+namespace {
+int convt_bwd_data_bnstats(const unet_view* x, int n, int h, int w, int cout, const float* kernel,
+                           const unsigned short* kernel_x3t, const float* dout, float* dx, const float* mean,
+                           const float* rstd, float* bn_partials, unet_stream_t stream) {
     if (check_view(x, "unet_conv_transpose2x2_bwd_data_bnstats")) return -1;
     const int S = unet_conv_transpose2x2_bwd_data_bnstats_slabs(x, n, h, w, cout);
     UNET_CHECK_ARG(S > 0, "unet_conv_transpose2x2_bwd_data_bnstats: needs a BNRELU view (dropout rate in [0, 1)) "
@@ -1965,6 +2086,8 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n
     a.uW = w;
     a.uf = cout;
     a.B = kernel;
+    // (split-precision route only where the partials are per 128-row tile, as the _slabs query said)
+    a.Bx = convt_bnpart_bm(a.M, cin) == 128 ? kernel_x3t : nullptr;
     a.sbk = cin;
     a.sbn = 1;
     a.N = cin;
@@ -1984,6 +2107,22 @@ extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n
     UNET_CHECK_ARG(rows_vec_ok(a, A_UNSHUFFLE) && ((uintptr_t)dx | (uintptr_t)x->src0) % 16 == 0,
                    "unet_conv_transpose2x2_bwd_data_bnstats: operands must be 16-B aligned");
     return launch_rows<A_UNSHUFFLE, false, E_BNPART>(a, as_stream(stream), "unet_conv_transpose2x2_bwd_data_bnstats");
+}
+}  // namespace
+
+extern "C" int unet_conv_transpose2x2_bwd_data_bnstats(const unet_view* x, int n, int h, int w, int cout,
+                                                       const float* kernel, const float* dout, float* dx,
+                                                       const float* mean, const float* rstd, float* bn_partials,
+                                                       unet_stream_t stream) {
+    return convt_bwd_data_bnstats(x, n, h, w, cout, kernel, nullptr, dout, dx, mean, rstd, bn_partials, stream);
+}
+extern "C" int unet_conv_transpose2x2_bwd_data_bnstats_x3(const unet_view* x, int n, int h, int w, int cout,
+                                                          const float* kernel, const unsigned short* kernel_x3t,
+                                                          const float* dout, float* dx, const float* mean,
+                                                          const float* rstd, float* bn_partials, unet_stream_t stream) {
+    UNET_CHECK_ARG(kernel_x3t && (uintptr_t)kernel_x3t % 16 == 0,
+                   "unet_conv_transpose2x2_bwd_data_bnstats_x3: kernel_x3t must be a 16-B aligned plane set");
+    return convt_bwd_data_bnstats(x, n, h, w, cout, kernel, kernel_x3t, dout, dx, mean, rstd, bn_partials, stream);
 }
 
 namespace unet {

@@ -393,6 +393,9 @@ struct SplitTable {
 };
 // dst planes [3][cols][rows] (bf16 bits) of src [rows][cols]: a 32 x 32 tile per block through LDS,
 // read along cols and written along rows (blockIdx.y = segment)
+// (KEEP: planes [3][rows][cols] in the source layout, for the operands a GEMM stages k-contiguous as
+// they are: the dgrad reads pw_kernel[ci][co] with k = co)
+template <bool KEEP>
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ src, SplitTable t,
                                                        unsigned short* __restrict__ dst) {
     __shared__ float T[32][33];
@@ -411,14 +414,16 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
         }
         __syncthreads();
         for (int i = threadIdx.x; i < 1024; i += 256) {
-            const int c = c0 + (i >> 5), r = r0 + (i & 31);
+            // transposed planes: consecutive threads walk r (the destination's contiguous axis);
+            // KEEP: they walk c, as the source
+            const int c = c0 + (KEEP ? (i & 31) : (i >> 5)), r = r0 + (KEEP ? (i >> 5) : (i & 31));
             if (r < rows && c < cols) {
-                const float x = T[i & 31][i >> 5];
+                const float x = T[r - r0][c - c0];
                 const unsigned h = bf16_bits(x);
                 const float rr = x - bf16_val(h);
                 const unsigned m = bf16_bits(rr);
                 const unsigned l = bf16_bits(rr - bf16_val(m));
-                const int64_t o = (int64_t)c * rows + r;
+                const int64_t o = KEEP ? (int64_t)r * cols + c : (int64_t)c * rows + r;
                 D[o] = (unsigned short)h;
                 D[plane + o] = (unsigned short)m;
                 D[2 * plane + o] = (unsigned short)l;
@@ -429,8 +434,8 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
 }  // namespace
 }  // namespace unet
 
-extern "C" int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
-                             unet_stream_t stream) {
+namespace {
+int split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst, unet_stream_t stream, bool keep) {
     UNET_CHECK_ARG(src && segs && dst && nseg > 0 && nseg <= UNET_SPLIT_MAX_SEGS, "unet_split_x3: bad arguments");
     unet::SplitTable t{};
     t.n = nseg;
@@ -447,10 +452,23 @@ extern "C" int unet_split_x3(const float* src, const int64_t* segs, int nseg, un
         const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
         if (tiles > maxtiles) maxtiles = tiles > 1024 ? 1024 : (int)tiles;
     }
-    unet::split_x3_kernel<<<dim3((unsigned)maxtiles, (unsigned)nseg), 256, 0, static_cast<hipStream_t>(stream)>>>(
-        src, t, dst);
+    const dim3 grid((unsigned)maxtiles, (unsigned)nseg);
+    if (keep)
+        unet::split_x3_kernel<true><<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(src, t, dst);
+    else
+        unet::split_x3_kernel<false><<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(src, t, dst);
     UNET_CHECK_LAUNCH("unet_split_x3");
     return 0;
+}
+}  // namespace
+
+extern "C" int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                             unet_stream_t stream) {
+    return split_x3(src, segs, nseg, dst, stream, false);
+}
+extern "C" int unet_split_x3_keep(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                                  unet_stream_t stream) {
+    return split_x3(src, segs, nseg, dst, stream, true);
 }
 
 extern "C" int unet_abi_version(void) { return UNET_ABI_VERSION; }

@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -57,12 +57,14 @@ SIGNATURES = {
     "unet_dwconv3x3_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "unet_bn_partials_size": (c_size_t, [c_int64, c_int]),
     "unet_pointwise_fwd": (c_int, [P, c_int64, c_int, c_int, P, P, P, P]),
+    "unet_pointwise_fwd_x3": (c_int, [P, c_int64, c_int, c_int, P, P, P, P, P]),
     "unet_pointwise_bwd_data": (c_int, [P, c_int64, c_int, c_int, P, P, P]),
     "unet_pointwise_bwd_filter_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_filter": (c_int, [P, P, c_int64, c_int, c_int, P, P, c_size_t, P]),
     "unet_sepconv_fwd_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_fwd": (c_int, [_VP, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P]),
     "unet_split_x3": (c_int, [P, P, c_int, P, P]),
+    "unet_split_x3_keep": (c_int, [P, P, c_int, P, P]),
     "unet_pool_select": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
@@ -84,6 +86,8 @@ SIGNATURES = {
                                        c_size_t, P]),
     "unet_pointwise_bwd_data_bnrelu": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, c_float, c_uint64, P, P,
                                                P]),
+    "unet_pointwise_bwd_data_bnrelu_x3": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, c_float, c_uint64, P,
+                                                  P, P]),
     "unet_pointwise_bwd_data_bnrelu_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int]),
     "unet_pointwise_bwd_data_bnrelu_wgrad": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, P, P, P, P, P, c_size_t,
                                                      P]),
@@ -91,10 +95,13 @@ SIGNATURES = {
     "unet_image_block_bwd_wgrad": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P,
                                            c_size_t, P]),
     "unet_conv_transpose2x2_fwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P]),
+    "unet_conv_transpose2x2_fwd_x3": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "unet_conv_transpose2x2_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "unet_conv_transpose2x2_bwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_size_t, P]),
     "unet_conv_transpose2x2_bwd_data_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_conv_transpose2x2_bwd_data_bnstats": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P]),
+    "unet_conv_transpose2x2_bwd_data_bnstats_x3": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P,
+                                                          P]),
     "unet_head_fwd": (c_int, [_VP, c_int, c_int, c_int, c_int, P, P, P, P]),
     "unet_dice_workspace": (c_size_t, [c_int, c_int64, c_int]),
     "unet_dice_fwd": (c_int, [P, P, c_int, c_int64, c_int, c_float, P, P, P, c_size_t, P]),

@@ -249,8 +249,36 @@ class UNetEngine:
         self.x3_live: set = set()
         self._x3_plans: Dict[int, tuple] = {}
         self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
+        # ... and the same kernels' planes in their own layout ([3][Cin][Cout], k = Cout contiguous)
+        # for the split-precision BatchNorm-backward data gradient (unet_pointwise_bwd_data_bnrelu_x3),
+        # refreshed by one launch per training forward: every block but the padded image block (the
+        # 64-output blocks that take the fused block backward do not read theirs)
+        self.x6_gemm = True
+        self.x3d_off: Dict[str, int] = {}
+        self.x3d_segs = []
+        offd = 0
+        for b in self.blocks:
+            if b.cout % 32 == 0 and b.cin % 4 == 0 and not b.wcin:
+                src = self.train_layout.offsets[f"{b.name}_sepconv/pointwise_kernel"]
+                self.x3d_segs.append((src, b.cin, b.cout, offd))
+                self.x3d_off[b.name] = offd
+                offd += (3 * b.cin * b.cout + 7) // 8 * 8
+        # the Conv2DTranspose kernels (2, 2, f, cin) seen as (4 f, cin): planes in their own layout for
+        # the forward (k = cin contiguous) and transposed ([3][cin][4 f]) for the data gradient
+        self.x3u_off: Dict[str, tuple] = {}
+        self.x3t_segs = []
+        offt = 0
+        for stage, fi, cin, _b1, _b2 in self.dec:
+            src = self.train_layout.offsets[f"{stage}_upsample/kernel"]
+            self.x3d_segs.append((src, 4 * fi, cin, offd))
+            self.x3t_segs.append((src, 4 * fi, cin, offt))
+            self.x3u_off[stage] = (offd, offt, 12 * fi * cin)
+            offd += (12 * fi * cin + 7) // 8 * 8
+            offt += (12 * fi * cin + 7) // 8 * 8
+        self.pkd = torch.empty(max(offd, 8), dtype=torch.int16, device=self.device)
+        self.pkt = torch.empty(max(offt, 8), dtype=torch.int16, device=self.device)
 
-    def _refresh_x3(self, n: int):
+    def _refresh_x3(self, n: int, training: bool = False):
         """Re-split on EVERY forward (one small launch): the planes then always match the fp32
         weights the backward reads, whatever wrote engine.params in between (AdamW, a custom
         optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast).  Only the
@@ -258,18 +286,44 @@ class UNetEngine:
         if not self.use_x3:
             self.x3_live = set()
             return
-        plan = self._x3_plans.get((n, self.fuse_min_total))
+        # (a training step with the split-precision GEMMs also refreshes the blocks whose forward is the
+        # depthwise launch + the pointwise GEMM: unet_pointwise_fwd_x3 reads the same planes)
+        every = training and self.x6_gemm
+        key = (n, self.fuse_min_total, every)
+        plan = self._x3_plans.get(key)
         if plan is None:  # (cached per batch size: the host loop is on the critical path of small steps)
             segs, live = [], set()
             for b, seg in self.x3_cand:
                 h, w = self._dims(b.level)
-                if h * w >= FUSE_MIN_PIXELS or n * h * w >= self.fuse_min_total:
+                if every or h * w >= FUSE_MIN_PIXELS or n * h * w >= self.fuse_min_total:
                     segs.append(seg)
                     live.add(b.name)
-            plan = self._x3_plans[(n, self.fuse_min_total)] = (segs, live)
+            plan = self._x3_plans[key] = (segs, live)
         segs, self.x3_live = plan
         if segs:
             ops.split_x3(self.params, segs, self.pkx)
+
+    def _refresh_x3d(self):
+        if self.x6_gemm and self.x3d_segs:
+            ops.split_x3(self.params, self.x3d_segs, self.pkd, keep=True)
+            ops.split_x3(self.params, self.x3t_segs, self.pkt)
+
+    def _ukx(self, stage: str, training: bool):
+        """The training forward's split-precision planes of an upsample kernel (None: fp32 route)."""
+        if not (self.x6_gemm and training):
+            return None
+        o, _, nel = self.x3u_off[stage]
+        return self.pkd[o:o + nel]
+
+    def _ukt(self, stage: str):
+        if not self.x6_gemm:
+            return None
+        _, o, nel = self.x3u_off[stage]
+        return self.pkt[o:o + nel]
+
+    def _pkd(self, b: "Block"):
+        o = self.x3d_off.get(b.name) if self.x6_gemm else None
+        return None if o is None else self.pkd[o:o + 3 * b.cin * b.cout]
 
     def _pkx(self, b: "Block"):
         o = self.x3_off.get(b.name) if self.use_x3 and b.name in self.x3_live else None
@@ -381,9 +435,9 @@ class UNetEngine:
         bb.y_recompute = False
         ops.dwconv3x3_fwd(view, n, h, w, dk, bb.y)
         if training and self.use_bn:
-            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, bb.part)
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, bb.part, pkx=self._pkx(b))
         else:
-            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, None)
+            ops.pointwise_fwd(bb.y, m, b.cin, b.cout, pk, bb.z, None, pkx=self._pkx(b))
         if bb.zsel is not None:
             ops.pool_select(bb.z, n, h, w, b.cout, gamma, bb.zsel)
         if training and self.use_bn:
@@ -484,7 +538,9 @@ class UNetEngine:
         if drop and seeds is None:
             seeds = self.drop_seeds(self.step_count + 1)
         x = self._padded_input(A, x)
-        self._refresh_x3(n)
+        self._refresh_x3(n, training)
+        if training:
+            self._refresh_x3d()
         self._x_fwd = x
         v = View.plain(x)
         for stage, b1, b2 in self.enc:
@@ -500,7 +556,7 @@ class UNetEngine:
         for i, (stage, fi, cin, b1, b2) in enumerate(self.dec):
             h, w = self._dims(b1.level + 1)
             ops.conv_transpose2x2_fwd(v, n, h, w, fi, self.vars[f"{stage}_upsample/kernel"],
-                                      self.vars[f"{stage}_upsample/bias"], A.up[stage])
+                                      self.vars[f"{stage}_upsample/bias"], A.up[stage], kx=self._ukx(stage, training))
             skip = A.blocks[self.enc[len(self.enc) - 1 - i][2].name]
             v = View.concat(A.up[stage], skip.z, skip.scale, skip.shift)
             if drop and i < len(self.dec) - 1:
@@ -655,7 +711,7 @@ class UNetEngine:
                                           dy, gdk_f, gpk_f)
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
-                                              drop_rate, drop_seed, dy, dz)
+                                              drop_rate, drop_seed, dy, dz, pkd=self._pkd(b))
         else:
             if self._sync_bn_on():
                 raise RuntimeError("SyncBN needs the fused BN-backward route (fuse_bn_bwd, channels % 4 == 0)")
@@ -768,7 +824,8 @@ class UNetEngine:
             if S > 0:
                 ops.conv_transpose2x2_bwd_data_bnstats(xv, n, h, w, fi, uk, A.dup[stage], pb.da,
                                                        pb.mean if self.use_bn else None,
-                                                       pb.rstd if self.use_bn else None, self._bnpart(pb, S, xv.c0))
+                                                       pb.rstd if self.use_bn else None, self._bnpart(pb, S, xv.c0),
+                                                       kxt=self._ukt(stage))
                 pb.bn_slabs = S
                 pb.bn_masked = xv.drop_rate > 0.0  # (the bottleneck's dropout: the partials carry its mask)
             else:

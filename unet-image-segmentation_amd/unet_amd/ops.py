@@ -144,6 +144,12 @@ def _ws(nbytes: int, device):
     return _ptr(buf), buf.numel()
 
 
+def _planes(t: Optional[Tensor], numel: int, what: str):
+    if t is not None and (t.dtype != torch.int16 or t.numel() < 3 * numel or not t.is_cuda):
+        raise ValueError(f"{what}: split-precision planes must be 3 x {numel} int16 on the device")
+    return t
+
+
 # ---------------------------------------------------------------------------- views ---
 @dataclass
 class View:
@@ -299,14 +305,20 @@ def bn_partials_numel(m: int, c: int) -> int:
     return L.query("unet_bn_partials_size", m, c) // 4
 
 
-def pointwise_fwd(y: Tensor, m: int, cin: int, cout: int, pk: Tensor, z: Tensor, partials: Optional[Tensor] = None):
+def pointwise_fwd(y: Tensor, m: int, cin: int, cout: int, pk: Tensor, z: Tensor, partials: Optional[Tensor] = None,
+                  pkx: Optional[Tensor] = None):
+    """pkx: pk's split-precision planes ([3][cout][cin], split_x3): the bf16x6 GEMM where cin % 32 == 0."""
     _check(y, "y", m * cin)
     _check(pk, "pointwise_kernel", cin * cout)
     _check(z, "z", m * cout)
     if partials is not None:
         _check(partials, "bn_partials", bn_partials_numel(m, cout))
-    _call("unet_pointwise_fwd", (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout)), _ptr(y), m, cin,
-          cout, _ptr(pk), _ptr(z), _ptr(partials), _stream())
+    work = (2.0 * m * cin * cout, 4.0 * (m * cin + m * cout + cin * cout))
+    if _planes(pkx, cin * cout, "pointwise_fwd") is not None:
+        _call("unet_pointwise_fwd_x3", work, _ptr(y), m, cin, cout, _ptr(pk), _ptr(pkx), _ptr(z), _ptr(partials),
+              _stream())
+        return
+    _call("unet_pointwise_fwd", work, _ptr(y), m, cin, cout, _ptr(pk), _ptr(z), _ptr(partials), _stream())
 
 
 def pointwise_bwd_data(dz: Tensor, m, cin, cout, pk: Tensor, dy: Tensor):
@@ -342,10 +354,11 @@ def sepconv_supported(x: View, n: int, h: int, w: int, cout: int) -> bool:
     return bool(L.load().unet_sepconv_fwd_supported(ctypes.byref(vs), n, h, w, cout))
 
 
-def split_x3(src: Tensor, segs, dst: Tensor):
+def split_x3(src: Tensor, segs, dst: Tensor, keep: bool = False):
     """bf16 x 3 split-precision planes of several weight matrices in one launch: segs = [(source
     offset, rows, cols, destination offset)] in elements of src (float32) / dst (int16 holding
-    bf16 bits); each segment becomes planes [3][cols][rows] at its destination offset."""
+    bf16 bits); each segment becomes planes [3][cols][rows] at its destination offset
+    (keep=True: [3][rows][cols], the source layout -- unet_split_x3_keep)."""
     if src.dtype != torch.float32 or dst.dtype != torch.int16:
         raise TypeError("split_x3: float32 source, int16 (bf16 bits) destination")
     flat = [int(v) for seg in segs for v in seg]
@@ -353,8 +366,8 @@ def split_x3(src: Tensor, segs, dst: Tensor):
         if so + r * c > src.numel() or do + 3 * r * c > dst.numel():
             raise ValueError("split_x3: segment out of range")
     arr = (ctypes.c_int64 * len(flat))(*flat)
-    _call("unet_split_x3", (0.0, sum(10.0 * r * c for _, r, c, _ in segs)), _ptr(src), arr, len(segs), _ptr(dst),
-          _stream())
+    _call("unet_split_x3_keep" if keep else "unet_split_x3", (0.0, sum(10.0 * r * c for _, r, c, _ in segs)),
+          _ptr(src), arr, len(segs), _ptr(dst), _stream())
 
 
 def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tensor, y: Optional[Tensor],
@@ -533,8 +546,10 @@ def bn_relu_bwd_stats_finish(partials: Tensor, S: int, m: int, c: int, mean, rst
 
 def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int, pk: Tensor, scale: Tensor,
                               shift: Tensor, coef: Tensor, drop_rate: float, drop_seed: int, dy: Tensor,
-                              dz: Optional[Tensor]):
-    """dy = dz . pk^T with dz (BN + ReLU + dropout backward) formed on load; optionally stores dz."""
+                              dz: Optional[Tensor], pkd: Optional[Tensor] = None):
+    """dy = dz . pk^T with dz (BN + ReLU + dropout backward) formed on load; optionally stores dz.
+    pkd: pk's split-precision planes in its own layout (split_x3(keep=True)): the bf16x6 GEMM
+    (unet_pointwise_bwd_data_bnrelu_x3) where cout % 32 == 0."""
     _check(da, "da", m * cout)
     _check(z, "z", m * cout)
     _check(pk, "pointwise_kernel", cin * cout)
@@ -545,8 +560,15 @@ def pointwise_bwd_data_bnrelu(da: Tensor, z: Tensor, m: int, cin: int, cout: int
     # (measurement label only) the library forms dz in a streaming pass and runs the plain GEMM
     # when either side has >= 1024 channels (gemm.hip, unet_pointwise_bwd_data_bnrelu)
     route = "dz_pass+gemm" if dz is not None and (cin >= 1024 or cout >= 1024) else "gemm_bnbwd"
-    _call("unet_pointwise_bwd_data_bnrelu",
-          (2.0 * m * cin * cout, 4.0 * (2 * m * cout + m * cin + cin * cout) + (4.0 * m * cout if dz is not None else 0)),
+    work = (2.0 * m * cin * cout, 4.0 * (2 * m * cout + m * cin + cin * cout) + (4.0 * m * cout if dz is not None else 0))
+    if pkd is not None:
+        if pkd.dtype != torch.int16 or pkd.numel() < 3 * cin * cout or not pkd.is_cuda:
+            raise ValueError("pointwise_bwd_data_bnrelu: pkd must be 3 x cin x cout int16 planes on the device")
+        _call("unet_pointwise_bwd_data_bnrelu_x3", work, _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(pkd),
+              _ptr(scale), _ptr(shift), _ptr(coef), float(drop_rate), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy),
+              _ptr(dz), _stream(), route=route + ("_x6" if cout % 32 == 0 else ""))
+        return
+    _call("unet_pointwise_bwd_data_bnrelu", work,
           _ptr(da), _ptr(z), m, cin, cout, _ptr(pk), _ptr(scale), _ptr(shift), _ptr(coef), float(drop_rate),
           int(drop_seed) & 0xFFFFFFFFFFFFFFFF, _ptr(dy), _ptr(dz), _stream(), route=route)
 
@@ -592,13 +614,20 @@ def image_block_bwd_wgrad(x: Tensor, n: int, h: int, w: int, wcin: int, cout: in
 
 
 # ------------------------------------------------------------ Conv2DTranspose ---
-def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor], out: Tensor):
+def conv_transpose2x2_fwd(x: View, n, h, w, cout, k: Tensor, b: Optional[Tensor], out: Tensor,
+                          kx: Optional[Tensor] = None):
+    """kx: k's split-precision planes in its own layout (split_x3(keep=True) of (4 cout, cin)): the
+    bf16x6 GEMM (unet_conv_transpose2x2_fwd_x3) where cin % 32 == 0."""
     _check(k, "kernel", 4 * cout * x.c0)
     _check(out, "out", n * 4 * h * w * cout)
     vs = x.c_struct()
     m = n * h * w
-    _call("unet_conv_transpose2x2_fwd", (8.0 * m * x.c0 * cout, 4.0 * (m * x.c0 + 4 * m * cout + 4 * x.c0 * cout)),
-          ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(b), _ptr(out), _stream())
+    work = (8.0 * m * x.c0 * cout, 4.0 * (m * x.c0 + 4 * m * cout + 4 * x.c0 * cout))
+    if _planes(kx, 4 * cout * x.c0, "conv_transpose2x2_fwd") is not None:
+        _call("unet_conv_transpose2x2_fwd_x3", work, ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(kx), _ptr(b),
+              _ptr(out), _stream())
+        return
+    _call("unet_conv_transpose2x2_fwd", work, ctypes.byref(vs), n, h, w, cout, _ptr(k), _ptr(b), _ptr(out), _stream())
 
 
 def conv_transpose2x2_bwd(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Optional[Tensor],
@@ -627,9 +656,10 @@ def conv_transpose2x2_bwd_data_bnstats_slabs(x: View, n, h, w, cout) -> int:
 
 
 def conv_transpose2x2_bwd_data_bnstats(x: View, n, h, w, cout, k: Tensor, dout: Tensor, dx: Tensor, mean, rstd,
-                                       partials: Tensor):
+                                       partials: Tensor, kxt: Optional[Tensor] = None):
     """Data gradient of conv_transpose2x2 (x: the BNRELU view of the block below, no dropout) that
-    also emits that block's BN-backward partials (finish: bn_relu_bwd_stats_finish)."""
+    also emits that block's BN-backward partials (finish: bn_relu_bwd_stats_finish).  kxt: k's
+    split-precision planes transposed (split_x3 of (4 cout, cin): [3][cin][4 cout]), the bf16x6 GEMM."""
     S = conv_transpose2x2_bwd_data_bnstats_slabs(x, n, h, w, cout)
     _check(dout, "dout", n * 4 * h * w * cout)
     _check(dx, "dx", n * h * w * x.c0)
@@ -637,6 +667,10 @@ def conv_transpose2x2_bwd_data_bnstats(x: View, n, h, w, cout, k: Tensor, dout: 
     vs = x.c_struct()
     m = n * h * w
     nb = 16.0 * m * cout + 8.0 * m * x.c0 + 16.0 * x.c0 * cout + 8.0 * S * x.c0
+    if _planes(kxt, 4 * cout * x.c0, "conv_transpose2x2_bwd_data_bnstats") is not None:
+        _call("unet_conv_transpose2x2_bwd_data_bnstats_x3", (8.0 * m * x.c0 * cout, nb), ctypes.byref(vs), n, h, w,
+              cout, _ptr(k), _ptr(kxt), _ptr(dout), _ptr(dx), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
+        return
     _call("unet_conv_transpose2x2_bwd_data_bnstats", (8.0 * m * x.c0 * cout, nb), ctypes.byref(vs), n, h, w, cout,
           _ptr(k), _ptr(dout), _ptr(dx), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
 
