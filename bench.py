@@ -337,6 +337,10 @@ def parse_args(argv=None):
                          "the fused block backward (A/B)")
     ap.add_argument("--fuse", choices=("auto", "always"), default="auto",
                     help="fused conv forward on the levels >= 64x64 (auto) or on every level (A/B)")
+    ap.add_argument("--fuse-min-pixels", type=int, default=0,
+                    help="fused conv forward from levels of this many pixels per image (0: the engine's rule; A/B)")
+    ap.add_argument("--fuse-min-total", type=int, default=0,
+                    help="... and on smaller levels from this many pixels per launch (0: the engine's rule; A/B)")
     ap.add_argument("--recompute-y128", action="store_true",
                     help="128-output blocks too: no y store, weight gradients recompute it (A/B)")
     ap.add_argument("--recompute-y64-128", action="store_true",
@@ -382,6 +386,10 @@ def main():
     model.engine.x6_gemm = not args.no_x6_gemm
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
+    if args.fuse_min_pixels:
+        model.engine.fuse_min_pixels = args.fuse_min_pixels
+    if args.fuse_min_total:
+        model.engine.fuse_min_total = args.fuse_min_total
     if args.recompute_y128:
         model.engine.recompute_y_couts = (64, 128)
     elif args.recompute_y64_128:

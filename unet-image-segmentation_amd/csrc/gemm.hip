@@ -1562,7 +1562,10 @@ WgradPlan wgrad_plan(int64_t M, int P, int Q) {
     return w;
 }
 
-// Split-precision weight gradients (both operands split as they are staged): 128 x 128 tiles.
+// Split-precision weight gradients (both operands split as they are staged, 128 x 128 tiles): lab
+// only.  Slower than fp32 MFMA on every train-step shape (0.71-0.99x isolated, step 10.80 vs 9.85 ms,
+// profiles/r6w_wgrad_x6_ab.txt): both operands pay the transpose + split VALU inside the 16-stage
+// slices of the split-K grid, with no pre-split operand to lean on.
 bool wgrad_x6() { return lab_knob("UNET_WGRAD_X6", 0) != 0; }
 
 template <int AMODE, bool ADROP, int BMODE, bool BDROP>

@@ -48,12 +48,13 @@ RECOMPUTE_Y_COUTS = (64,)
 
 
 def block_fwd_choice(view: View, n: int, h: int, w: int, cout: int, training: bool, fuse: str = "auto",
-                     recompute_y: bool = True, recompute_couts=RECOMPUTE_Y_COUTS, min_total: int = FUSE_MIN_TOTAL_PIXELS):
+                     recompute_y: bool = True, recompute_couts=RECOMPUTE_Y_COUTS, min_total: int = FUSE_MIN_TOTAL_PIXELS,
+                     min_pixels: int = FUSE_MIN_PIXELS):
     """The kernels a conv_block forward runs: (fused, keep_y).  fused: one unet_sepconv_fwd launch
     (else unet_dwconv3x3_fwd + unet_pointwise_fwd, which always store y); keep_y: the fused launch
     also stores the depthwise output y for the weight gradients (training blocks whose weight
     gradients do not recompute it).  Shared by the engine and bench.py's encoder table."""
-    want = fuse == "always" or (fuse == "auto" and (h * w >= FUSE_MIN_PIXELS or n * h * w >= min_total))
+    want = fuse == "always" or (fuse == "auto" and (h * w >= min_pixels or n * h * w >= min_total))
     if not (want and ops.sepconv_supported(view, n, h, w, cout)):
         return False, training
     y_recompute = training and recompute_y and (cout in recompute_couts or (view.channels, cout) in recompute_couts) and \
@@ -178,7 +179,8 @@ class UNetEngine:
         # where it measured faster (levels of >= 64x64 pixels, tools/bench_sepconv.py and
         # profiles/r1i_sepconv_bn_sweep.log); "always" / "never" force the choice (tests).
         self.fuse_sepconv = "auto"
-        self.fuse_min_total = FUSE_MIN_TOTAL_PIXELS  # ... and below 64 x 64 from this many pixels per launch
+        self.fuse_min_pixels = FUSE_MIN_PIXELS  # levels of at least this many pixels per image ...
+        self.fuse_min_total = FUSE_MIN_TOTAL_PIXELS  # ... and below that from this many pixels per launch
         # BN + ReLU backward folded into the pointwise data-gradient GEMM (no separate dz pass)
         self.fuse_bn_bwd = True
         # BN-backward statistics of a block emitted by the launch that completes its da (the next
@@ -289,13 +291,13 @@ class UNetEngine:
         # (a training step with the split-precision GEMMs also refreshes the blocks whose forward is the
         # depthwise launch + the pointwise GEMM: unet_pointwise_fwd_x3 reads the same planes)
         every = training and self.x6_gemm
-        key = (n, self.fuse_min_total, every)
+        key = (n, self.fuse_min_pixels, self.fuse_min_total, every)
         plan = self._x3_plans.get(key)
         if plan is None:  # (cached per batch size: the host loop is on the critical path of small steps)
             segs, live = [], set()
             for b, seg in self.x3_cand:
                 h, w = self._dims(b.level)
-                if every or h * w >= FUSE_MIN_PIXELS or n * h * w >= self.fuse_min_total:
+                if every or h * w >= self.fuse_min_pixels or n * h * w >= self.fuse_min_total:
                     segs.append(seg)
                     live.add(b.name)
             plan = self._x3_plans[key] = (segs, live)
@@ -419,7 +421,7 @@ class UNetEngine:
         gamma, beta, mm, mv = self._bn(b.name)
         dk, pk = self._wts(b)
         fused, keep_y = block_fwd_choice(view, n, h, w, b.cout, training, self.fuse_sepconv, self.recompute_y,
-                                         self.recompute_y_couts, self.fuse_min_total)
+                                         self.recompute_y_couts, self.fuse_min_total, self.fuse_min_pixels)
         if fused:
             # one kernel: depthwise taps computed into the GEMM's A tile; y kept for the weight
             # grads unless they recompute it from the view
