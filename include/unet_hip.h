@@ -91,7 +91,7 @@ int unet_copy_strided(const float* src, int64_t rows, int cols, int64_t src_ld, 
  * planes [3][cols][rows] (transposed) with src[r][c] == hi + mid + lo exactly (round-to-nearest
  * bf16 of the value, then of each remainder).  One launch for every pointwise kernel of a step.
  * dst offsets must be multiples of 8 (16-B planes); rows * cols per plane.                  */
-#define UNET_SPLIT_MAX_SEGS 32
+#define UNET_SPLIT_MAX_SEGS 64
 int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
                   unet_stream_t stream);
 /* The same split with the planes in the source layout, [3][rows][cols] (ABI 12): the operand
@@ -99,6 +99,11 @@ int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned shor
  * pw_kernel (Cin, Cout) with k = Cout contiguous).                                            */
 int unet_split_x3_keep(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
                        unet_stream_t stream);
+/* Both layouts in one launch: segs[5 i .. 5 i + 4] = source offset, rows, cols, destination
+ * offset, keep (non-zero: [3][rows][cols], else [3][cols][rows]); the train step's one split per
+ * weight update (ABI 12).                                                                      */
+int unet_split_x3_mixed(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                        unet_stream_t stream);
 
 /* Writes the logical tensor of a view, out (n, h, w, c0 + c1): the activation relu(bn(z)),
  * its max-pool, or the (dropped-out) concat.  The training path never needs this (consumers

@@ -38,8 +38,9 @@ def _planes(ops, w2d: np.ndarray, keep: bool):
 
 
 def _tiles(m: int, n: int) -> int:
-    """128 x 128 tiles of an (m, n) output: the split-precision route needs >= 256 (gemm.hip rows_x6)"""
-    return (m + 127) // 128 * ((n + 127) // 128)
+    """128 x 128 tiles of an (m, n) output: the split-precision route needs >= 256 of them and n > 64
+    (gemm.hip rows_x6)"""
+    return 0 if n <= 64 else (m + 127) // 128 * ((n + 127) // 128)
 
 
 def _bf16(bits: np.ndarray) -> np.ndarray:
@@ -70,7 +71,7 @@ def _bnbwd_case(rng, m, cout, use_bn=True):
 
 @pytest.mark.parametrize("drop", [0.0, 0.2])
 @pytest.mark.parametrize("m,cin,cout", [(33000, 96, 128), (16384, 256, 256), (33000, 512, 64), (33000, 128, 1024),
-                                        (33000, 64, 48), (4096, 512, 256)])
+                                        (33000, 64, 48), (4096, 512, 256), (33000, 64, 128), (40000, 40, 64)])
 def test_pointwise_bwd_data_bnrelu_x3(ops, drop, m, cin, cout):
     """dy = dz . pk^T with dz formed on load: the split-precision route within TOL of float64 of the
     same dz; cout = 1024 takes the streaming-dz route + the plain split-precision GEMM; cout = 48 (k
@@ -230,3 +231,17 @@ def test_conv_transpose_bwd_filter_x6(ops, drop, n, h, w, cin, cout):
     rdk = np.einsum("niajbd,nijc->abdc", d6, x)
     assert rel_err(host(dk), rdk) < TOL
     assert rel_err(host(db), d6.sum((0, 1, 2, 3, 4))) < 1e-5
+
+
+def test_split_x3_mixed(ops):
+    """One mixed-layout launch (unet_split_x3_mixed, the train step's per-forward refresh) writes the
+    same planes as the two single-layout launches."""
+    rng = np.random.default_rng(77)
+    src = dev(f32(rng.standard_normal(5000)))
+    segs = [(0, 40, 30, 0, 1), (1200, 16, 48, 3600, 0), (2000, 33, 17, 6000, 1)]
+    mixed = torch.zeros(8000, dtype=torch.int16, device="cuda")
+    ops.split_x3(src, segs, mixed)
+    ref = torch.zeros(8000, dtype=torch.int16, device="cuda")
+    for so, r, c, do, k in segs:
+        ops.split_x3(src, [(so, r, c, do)], ref, keep=bool(k))
+    assert torch.equal(mixed, ref)

@@ -19,7 +19,7 @@ PEAK = 157.3
 B = int(os.environ.get("B", 16))
 DROP = float(os.environ.get("DROP", 0.0))
 TAG = sys.argv[1] if len(sys.argv) > 1 else "x6"
-DGRAD = [("enc2_block2", 128, 128, 128), ("enc3_block1", 64, 128, 256), ("enc3_block2", 64, 256, 256),
+DGRAD = [("enc2_block1", 128, 64, 128), ("enc2_block2", 128, 128, 128), ("enc3_block1", 64, 128, 256), ("enc3_block2", 64, 256, 256),
          ("enc4_block1", 32, 256, 512), ("enc4_block2", 32, 512, 512), ("bneck_block1", 16, 512, 1024),
          ("dec4_block2", 32, 512, 512), ("dec3_block1", 64, 512, 256), ("dec3_block2", 64, 256, 256),
          ("dec2_block1", 128, 256, 128), ("dec2_block2", 128, 128, 128)]

@@ -1474,9 +1474,11 @@ void launch_rows_tile(const RowsArgs& a, hipStream_t st) {
 // a double buffer at one block per CU -- was load-latency bound and no faster than fp32 MFMA,
 // profiles/r3_x6_rows_ab.jsonl; lab UNET_X6 = 0 turns the route off for A/B runs.)
 // Grids of fewer than 256 128 x 128 tiles keep the fp32 route, whose narrow tiles fill the chip (the
-// bottleneck's data gradient at batch 16, 32 x 4 tiles: 61 vs 77 us, profiles/r6x_rows_x6.txt).
+// bottleneck's data gradient at batch 16, 32 x 4 tiles: 61 vs 77 us, profiles/r6x_rows_x6.txt), and so
+// do outputs of <= 64 columns (enc2_block1's data gradient: 98 us, 110 with 128-column split tiles
+// half masked, 110 with 64-column ones, profiles/r6v2_x6_n64.txt).
 bool rows_x6(const RowsArgs& a, int amode) {
-    return a.Bx != nullptr && a.K % 32 == 0 && (amode != A_BNBWD || a.K <= 512) &&
+    return a.Bx != nullptr && a.K % 32 == 0 && a.N > 64 && (amode != A_BNBWD || a.K <= 512) &&
            cdiv(a.M, 128) * cdiv(a.N, 128) >= lab_knob("UNET_X6_MIN_TILES", 256) && lab_knob("UNET_X6", 1) != 0;
 }
 

@@ -390,16 +390,17 @@ struct SplitTable {
     int n;
     int64_t src[UNET_SPLIT_MAX_SEGS], dst[UNET_SPLIT_MAX_SEGS];
     int rows[UNET_SPLIT_MAX_SEGS], cols[UNET_SPLIT_MAX_SEGS];
+    unsigned char keep[UNET_SPLIT_MAX_SEGS];  // per segment: planes in the source layout (else transposed)
 };
 // dst planes [3][cols][rows] (bf16 bits) of src [rows][cols]: a 32 x 32 tile per block through LDS,
 // read along cols and written along rows (blockIdx.y = segment)
 // (KEEP: planes [3][rows][cols] in the source layout, for the operands a GEMM stages k-contiguous as
 // they are: the dgrad reads pw_kernel[ci][co] with k = co)
-template <bool KEEP>
 __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ src, SplitTable t,
                                                        unsigned short* __restrict__ dst) {
     __shared__ float T[32][33];
     const int s = blockIdx.y;
+    const bool KEEP = t.keep[s] != 0;  // (uniform per block)
     const int rows = t.rows[s], cols = t.cols[s];
     const int tr = (rows + 31) / 32, tc = (cols + 31) / 32;
     const float* S = src + t.src[s];
@@ -435,13 +436,15 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
 }  // namespace unet
 
 namespace {
-int split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst, unet_stream_t stream, bool keep) {
+// keep: 0 every segment transposed, 1 every segment kept, -1 per segment (segs of 5: ..., keep flag)
+int split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst, unet_stream_t stream, int keep) {
+    const int F = keep < 0 ? 5 : 4;
     UNET_CHECK_ARG(src && segs && dst && nseg > 0 && nseg <= UNET_SPLIT_MAX_SEGS, "unet_split_x3: bad arguments");
     unet::SplitTable t{};
     t.n = nseg;
     int maxtiles = 1;
     for (int i = 0; i < nseg; ++i) {
-        const int64_t so = segs[4 * i], rows = segs[4 * i + 1], cols = segs[4 * i + 2], doff = segs[4 * i + 3];
+        const int64_t so = segs[F * i], rows = segs[F * i + 1], cols = segs[F * i + 2], doff = segs[F * i + 3];
         UNET_CHECK_ARG(so >= 0 && doff >= 0 && rows > 0 && cols > 0 && rows < (1 << 30) && cols < (1 << 30),
                        "unet_split_x3: bad segment %d", i);
         UNET_CHECK_ARG(doff % 8 == 0, "unet_split_x3: segment %d destination must be 16-B aligned", i);
@@ -449,14 +452,12 @@ int split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* ds
         t.dst[i] = doff;
         t.rows[i] = (int)rows;
         t.cols[i] = (int)cols;
+        t.keep[i] = (unsigned char)(keep < 0 ? segs[F * i + 4] != 0 : keep);
         const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
         if (tiles > maxtiles) maxtiles = tiles > 1024 ? 1024 : (int)tiles;
     }
     const dim3 grid((unsigned)maxtiles, (unsigned)nseg);
-    if (keep)
-        unet::split_x3_kernel<true><<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(src, t, dst);
-    else
-        unet::split_x3_kernel<false><<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(src, t, dst);
+    unet::split_x3_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(src, t, dst);
     UNET_CHECK_LAUNCH("unet_split_x3");
     return 0;
 }
@@ -464,11 +465,15 @@ int split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* ds
 
 extern "C" int unet_split_x3(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
                              unet_stream_t stream) {
-    return split_x3(src, segs, nseg, dst, stream, false);
+    return split_x3(src, segs, nseg, dst, stream, 0);
 }
 extern "C" int unet_split_x3_keep(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
                                   unet_stream_t stream) {
-    return split_x3(src, segs, nseg, dst, stream, true);
+    return split_x3(src, segs, nseg, dst, stream, 1);
+}
+extern "C" int unet_split_x3_mixed(const float* src, const int64_t* segs, int nseg, unsigned short* dst,
+                                   unet_stream_t stream) {
+    return split_x3(src, segs, nseg, dst, stream, -1);
 }
 
 extern "C" int unet_abi_version(void) { return UNET_ABI_VERSION; }

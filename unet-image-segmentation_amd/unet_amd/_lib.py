@@ -13,6 +13,7 @@ from pathlib import Path
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
 ABI_VERSION = 12
+SPLIT_MAX_SEGS = 64  # UNET_SPLIT_MAX_SEGS
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
 LOSS_DICE, LOSS_IOU = 0, 1
@@ -65,6 +66,7 @@ SIGNATURES = {
     "unet_sepconv_fwd": (c_int, [_VP, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P]),
     "unet_split_x3": (c_int, [P, P, c_int, P, P]),
     "unet_split_x3_keep": (c_int, [P, P, c_int, P, P]),
+    "unet_split_x3_mixed": (c_int, [P, P, c_int, P, P]),
     "unet_pool_select": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "unet_sepconv_bwd_filter_supported": (c_int, [_VP, c_int, c_int, c_int, c_int]),
     "unet_sepconv_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),

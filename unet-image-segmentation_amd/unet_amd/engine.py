@@ -250,7 +250,6 @@ class UNetEngine:
                 off += (3 * b.cin * b.cout + 7) // 8 * 8
         self.x3_live: set = set()
         self._x3_plans: Dict[int, tuple] = {}
-        self.pkx = torch.empty(max(off, 8), dtype=torch.int16, device=self.device)
         # ... and the same kernels' planes in their own layout ([3][Cin][Cout], k = Cout contiguous)
         # for the split-precision BatchNorm-backward data gradient (unet_pointwise_bwd_data_bnrelu_x3),
         # refreshed by one launch per training forward: every block but the padded image block (the
@@ -277,38 +276,40 @@ class UNetEngine:
             self.x3u_off[stage] = (offd, offt, 12 * fi * cin)
             offd += (12 * fi * cin + 7) // 8 * 8
             offt += (12 * fi * cin + 7) // 8 * 8
-        self.pkd = torch.empty(max(offd, 8), dtype=torch.int16, device=self.device)
-        self.pkt = torch.empty(max(offt, 8), dtype=torch.int16, device=self.device)
+        # one arena, so a training forward refreshes all three plane sets in ONE unet_split_x3_mixed launch
+        off, offd, offt = (max(v, 8) for v in (off, offd, offt))
+        self.x3buf = torch.empty(off + offd + offt, dtype=torch.int16, device=self.device)
+        self.pkx = self.x3buf[:off]
+        self.pkd = self.x3buf[off:off + offd]
+        self.pkt = self.x3buf[off + offd:]
+        self.x3_mixed = [(so, r, c, do + off, 1) for so, r, c, do in self.x3d_segs] + \
+                        [(so, r, c, do + off + offd, 0) for so, r, c, do in self.x3t_segs]
 
     def _refresh_x3(self, n: int, training: bool = False):
         """Re-split on EVERY forward (one small launch): the planes then always match the fp32
         weights the backward reads, whatever wrote engine.params in between (AdamW, a custom
         optimizer loop, an in-place edit of engine.vars, a data-parallel broadcast).  Only the
         blocks whose level the batch of n images fuses (block_fwd_choice's pixel rule)."""
-        if not self.use_x3:
-            self.x3_live = set()
-            return
         # (a training step with the split-precision GEMMs also refreshes the blocks whose forward is the
-        # depthwise launch + the pointwise GEMM: unet_pointwise_fwd_x3 reads the same planes)
-        every = training and self.x6_gemm
-        key = (n, self.fuse_min_pixels, self.fuse_min_total, every)
+        # depthwise launch + the pointwise GEMM -- unet_pointwise_fwd_x3 reads the same planes -- and the
+        # rows GEMMs' own planes, pkd / pkt: one mixed-layout launch for all of them)
+        six = training and self.x6_gemm
+        key = (n, self.fuse_min_pixels, self.fuse_min_total, six, self.use_x3)
         plan = self._x3_plans.get(key)
         if plan is None:  # (cached per batch size: the host loop is on the critical path of small steps)
             segs, live = [], set()
-            for b, seg in self.x3_cand:
-                h, w = self._dims(b.level)
-                if every or h * w >= self.fuse_min_pixels or n * h * w >= self.fuse_min_total:
-                    segs.append(seg)
-                    live.add(b.name)
+            if self.use_x3:
+                for b, seg in self.x3_cand:
+                    h, w = self._dims(b.level)
+                    if six or h * w >= self.fuse_min_pixels or n * h * w >= self.fuse_min_total:
+                        segs.append(seg + (0,))
+                        live.add(b.name)
+            if six:
+                segs += self.x3_mixed
             plan = self._x3_plans[key] = (segs, live)
         segs, self.x3_live = plan
         if segs:
-            ops.split_x3(self.params, segs, self.pkx)
-
-    def _refresh_x3d(self):
-        if self.x6_gemm and self.x3d_segs:
-            ops.split_x3(self.params, self.x3d_segs, self.pkd, keep=True)
-            ops.split_x3(self.params, self.x3t_segs, self.pkt)
+            ops.split_x3(self.params, segs, self.x3buf)
 
     def _ukx(self, stage: str, training: bool):
         """The training forward's split-precision planes of an upsample kernel (None: fp32 route)."""
@@ -541,8 +542,6 @@ class UNetEngine:
             seeds = self.drop_seeds(self.step_count + 1)
         x = self._padded_input(A, x)
         self._refresh_x3(n, training)
-        if training:
-            self._refresh_x3d()
         self._x_fwd = x
         v = View.plain(x)
         for stage, b1, b2 in self.enc:

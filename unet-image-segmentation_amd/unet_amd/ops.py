@@ -358,16 +358,20 @@ def split_x3(src: Tensor, segs, dst: Tensor, keep: bool = False):
     """bf16 x 3 split-precision planes of several weight matrices in one launch: segs = [(source
     offset, rows, cols, destination offset)] in elements of src (float32) / dst (int16 holding
     bf16 bits); each segment becomes planes [3][cols][rows] at its destination offset
-    (keep=True: [3][rows][cols], the source layout -- unet_split_x3_keep)."""
+    (keep=True: [3][rows][cols], the source layout -- unet_split_x3_keep).  Segments of five
+    (..., keep flag) mix both layouts in one launch (unet_split_x3_mixed)."""
     if src.dtype != torch.float32 or dst.dtype != torch.int16:
         raise TypeError("split_x3: float32 source, int16 (bf16 bits) destination")
+    mixed = len(segs) > 0 and len(segs[0]) == 5
+    if len(segs) > L.SPLIT_MAX_SEGS or any(len(sg) != (5 if mixed else 4) for sg in segs):
+        raise ValueError("split_x3: bad segment list")
     flat = [int(v) for seg in segs for v in seg]
-    for so, r, c, do in segs:
+    for so, r, c, do, *_ in segs:
         if so + r * c > src.numel() or do + 3 * r * c > dst.numel():
             raise ValueError("split_x3: segment out of range")
     arr = (ctypes.c_int64 * len(flat))(*flat)
-    _call("unet_split_x3_keep" if keep else "unet_split_x3", (0.0, sum(10.0 * r * c for _, r, c, _ in segs)),
-          _ptr(src), arr, len(segs), _ptr(dst), _stream())
+    name = "unet_split_x3_mixed" if mixed else ("unet_split_x3_keep" if keep else "unet_split_x3")
+    _call(name, (0.0, sum(10.0 * sg[1] * sg[2] for sg in segs)), _ptr(src), arr, len(segs), _ptr(dst), _stream())
 
 
 def sepconv_fwd(x: View, n: int, h: int, w: int, dk: Tensor, cout: int, pk: Tensor, y: Optional[Tensor],
