@@ -144,6 +144,19 @@ int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h, int w,
                                     float* dx0, const float* mean,
                                     const float* rstd, float* bn_partials,
                                     unet_stream_t stream);
+/* The same for a BNRELU view without dropout (round 6, ABI 12) that ALSO accumulates the
+ * layer's depthwise FILTER gradient from the same registers (d_dw[t][c] = sum_q x[q] dy[q - off(t)],
+ * x[q] = relu(z sc + sh) from the z the statistics read anyway): per tile a fixed-order [9][C]
+ * slab into dw_partials ([S][9][C], S = _slabs(...)); unet_reduce_slabs(dw_partials, S, 9 C,
+ * d_dw_kernel) sums them in tile order.  Replaces unet_dwconv3x3_bwd_filter's second pass over
+ * dy and the view for such a block (model/u_net.py:14-20, the GradientTape's depthwise gradient). */
+int unet_dwconv3x3_bwd_data_bnstats_dwf(const unet_view* x, int n, int h, int w,
+                                        const float* dw_kernel, const float* dy, float* dx0,
+                                        const float* mean, const float* rstd, float* bn_partials,
+                                        float* dw_partials, unet_stream_t stream);
+/* out[l] = sum_{s < S} slabs[s * len + l], summed in a fixed order (deterministic); slabs is
+ * scratch (overwritten).  The reduction of unet_dwconv3x3_bwd_data_bnstats_dwf's slabs.        */
+int unet_reduce_slabs(float* slabs, int S, int64_t len, float* out, unet_stream_t stream);
 
 size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c);
 /* d_dw_kernel (3,3,C,1) = sum over pixels of x(shifted) * dy (overwrites). */

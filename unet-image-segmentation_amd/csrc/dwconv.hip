@@ -383,7 +383,7 @@ int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W
 bool dw_tiled_ok(int C);
 int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
                               const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
-                              hipStream_t st);
+                              hipStream_t st, float* dwpart = nullptr);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
 
 static int check_dims(const unet_view* x, int n, int h, int w, const char* op) {
@@ -464,6 +464,26 @@ extern "C" int unet_dwconv3x3_bwd_data_bnstats(const unet_view* x, int n, int h,
     const DView v = make_dview(*x);
     return dw_tiled_bwd_data_bnstats(v, x->mode, x->drop_rate > 0.f, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
                                      as_stream(stream));
+}
+
+extern "C" int unet_dwconv3x3_bwd_data_bnstats_dwf(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                                                   const float* dy, float* dx0, const float* mean, const float* rstd,
+                                                   float* bn_partials, float* dw_partials, unet_stream_t stream) {
+    const char* op = "unet_dwconv3x3_bwd_data_bnstats_dwf";
+    if (check_view(x, op) || check_dims(x, n, h, w, op)) return -1;
+    UNET_CHECK_ARG(dw_kernel && dy && dx0 && bn_partials && dw_partials, "%s: null pointer", op);
+    UNET_CHECK_ARG(x->mode == UNET_VIEW_BNRELU && x->drop_rate == 0.f && unet_dwconv3x3_bwd_data_bnstats_slabs(x, n, h, w) > 0,
+                   "%s: needs a BNRELU view without dropout, channels %% 4 == 0 (tiled path)", op);
+    UNET_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "%s: mean and rstd go together", op);
+    UNET_CHECK_ARG((uintptr_t)dw_partials % 16 == 0, "%s: dw_partials must be 16-B aligned", op);
+    const DView v = make_dview(*x);
+    return dw_tiled_bwd_data_bnstats(v, x->mode, false, n, h, w, dw_kernel, dy, dx0, mean, rstd, bn_partials,
+                                     as_stream(stream), dw_partials);
+}
+
+extern "C" int unet_reduce_slabs(float* slabs, int S, int64_t len, float* out, unet_stream_t stream) {
+    UNET_CHECK_ARG(slabs && out && S > 0 && len > 0, "unet_reduce_slabs: bad arguments");
+    return reduce_slabs(slabs, S, len, out, len, len, as_stream(stream));
 }
 
 extern "C" size_t unet_dwconv3x3_bwd_filter_workspace(int n, int h, int w, int c) {

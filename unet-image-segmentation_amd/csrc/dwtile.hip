@@ -20,7 +20,7 @@ int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, 
 size_t dw_tiled_filter_partials(int N, int H, int W, int C);
 int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
                               const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
-                              hipStream_t st);
+                              hipStream_t st, float* dwpart = nullptr);
 size_t dw_tiled_ntiles(int N, int H, int W, int C);
 int dw_tiled_bwd_filter(const DView& v, int mode, bool drop, int N, int H, int W, const float* dY, float* part,
                         int* S_out, hipStream_t st);
@@ -175,19 +175,28 @@ __global__ __launch_bounds__(256, 3) void dw_tile_fwd(DView v, int N, int H, int
     }
 }
 
+// DWF (BNRELU view with STATS, no dropout): the depthwise FILTER gradient of the same layer from the
+// same registers: dK[t][c] = sum_p x[p + off(t)] dy[p] = sum_q x[q] dy[q - off(t)] (both zero outside
+// the image), and for the lane's output pixel q the staged dy window holds dy[q - off(t)] at
+// a[2 - i][2 - j] (t = 3 i + j) while x[q] = relu(z sc + sh) comes from the z the statistics read
+// anyway: 9 FMAs per element on the HBM-bound pass instead of a second pass over dy and the view
+// (round 6).  Per tile a fixed-order [9][C] slab (xor shuffles over the wave's columns, then the
+// four waves in order) into dwpart[tile]; unet_reduce_slabs sums the tiles in order.
 // STATS (POOL or BNRELU view): this kernel is the last writer of the view's block's da (POOL: it
 // adds the pooled half to the stored skip half and reads the block's raw z for the argmax anyway;
 // BNRELU: it writes the whole da and reads z for the mask), so it also emits that block's
 // BatchNorm-backward partial sums over its tile: bnpart[tile][0][c] = sum g,
 // bnpart[tile][1][c] = sum g * xhat with g = da * [z*sc+sh > 0], xhat = (z - mu) * rs (the
 // unet_bn_relu_bwd_stats reduction, without its separate pass over (da, z)).
-template <int MODE, bool DROP, int QT, bool STATS = false>
-__global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
+template <int MODE, bool DROP, int QT, bool STATS = false, bool DWF = false>
+__global__ __launch_bounds__(256, DWF ? 2 : 3) void dw_tile_bwd_data(DView v, int N, int H, int W, int tiles_w, int tiles_h,
                                                         const float* __restrict__ K, const float* __restrict__ dY,
                                                         float* __restrict__ dx0, float* __restrict__ dx1,
                                                         const float* __restrict__ mu = nullptr,
                                                         const float* __restrict__ rs = nullptr,
-                                                        float* __restrict__ bnpart = nullptr) {
+                                                        float* __restrict__ bnpart = nullptr,
+                                                        float* __restrict__ dwpart = nullptr) {
+    static_assert(!DWF || (STATS && MODE == UNET_VIEW_BNRELU && !DROP), "DWF: BNRELU view, statistics, no dropout");
     main_stream_prio();
     using G = Geom<QT>;
     __shared__ float4 T[G::NE];
@@ -217,6 +226,14 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
         }
     }
     float4 a[3][3];
+    float4 fk[DWF ? 9 : 1];  // DWF: this lane's filter-gradient sums
+    float4 xsc = f4(1.f), xsh = f4(0.f);
+    if constexpr (DWF) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) fk[t] = f4(0.f);
+        xsc = ld4(v.sc0 + c);
+        xsh = ld4(v.sh0 + c);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -230,6 +247,17 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
         for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) acc = fma4(a[i][j], kf[i * 3 + j], acc);
+        float4 zq = f4(0.f);
+        if constexpr (DWF) {  // x[q] (zero past the image) against the window's dy[q - off(t)]
+            const bool in = w < W && h0 + r < H;
+            zq = ld4(v.src0 + (in ? ((int64_t)(n * H + h0 + r) * W + w) * C + c : 0));
+            float4 xq = bnrelu4(zq, xsc, xsh);
+            if (!in) xq = f4(0.f);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) fk[i * 3 + j] = fma4(xq, a[2 - i][2 - j], fk[i * 3 + j]);
+        }
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             a[0][j] = a[1][j];
@@ -245,7 +273,7 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
         if constexpr (MODE == UNET_VIEW_PLAIN || MODE == UNET_VIEW_BNRELU) {
             st4(dx0 + (int64_t)p * C + c, acc);
             if constexpr (STATS && MODE == UNET_VIEW_BNRELU) {  // dx0 is the whole da of the view's block
-                const float4 zr = ld4(v.src0 + (int64_t)p * C + c);
+                const float4 zr = DWF ? zq : ld4(v.src0 + (int64_t)p * C + c);
                 const float4 sc = ld4(v.sc0 + c), sh = ld4(v.sh0 + c);
                 const float4 gm = make_float4(fmaf(zr.x, sc.x, sh.x) > 0.f ? acc.x : 0.f,
                                               fmaf(zr.y, sc.y, sh.y) > 0.f ? acc.y : 0.f,
@@ -303,6 +331,31 @@ __global__ __launch_bounds__(256, 3) void dw_tile_bwd_data(DView v, int N, int H
                     s2 = fma4(gm, xh, s2);
                 }
             }
+        }
+    }
+    if constexpr (DWF) {  // the tile's [9][C] filter-gradient slab: the wave's columns by xor shuffles
+        float4* R = T;    // (lanes l, l ^ QT, ...: one channel quad), then the four waves in order
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        __syncthreads();  // (every lane's window reads of T are done)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            float4 s = fk[t];
+#pragma unroll
+            for (int o = QT; o < 64; o <<= 1) {
+                s.x += __shfl_xor(s.x, o, 64);
+                s.y += __shfl_xor(s.y, o, 64);
+                s.z += __shfl_xor(s.z, o, 64);
+                s.w += __shfl_xor(s.w, o, 64);
+            }
+            if (lane < QT) R[(wv * 9 + t) * QT + lane] = s;
+        }
+        __syncthreads();
+        float* out = dwpart + (int64_t)tile * 9 * C;
+        for (int e = threadIdx.x; e < 9 * QT; e += 256) {
+            const int t = e / QT, qq = e - t * QT;
+            const float4 s = add4(add4(R[t * QT + qq], R[(9 + t) * QT + qq]),
+                                  add4(R[(18 + t) * QT + qq], R[(27 + t) * QT + qq]));
+            st4(out + t * C + cbase + 4 * qq, s);
         }
     }
     if constexpr (STATS) {  // fixed-order reduction over the TW column lanes of each channel quad
@@ -483,9 +536,26 @@ int dw_tiled_bwd_data(const DView& v, int mode, bool drop, int N, int H, int W, 
 
 int dw_tiled_bwd_data_bnstats(const DView& v, int mode, bool drop, int N, int H, int W, const float* K,
                               const float* dY, float* dx0, const float* mu, const float* rs, float* bnpart,
-                              hipStream_t st) {
+                              hipStream_t st, float* dwpart) {
     TilePlan p = tile_plan(N, H, W, v.C);
     dim3 grid((unsigned)p.ntiles, (unsigned)p.chunks);
+    if (dwpart) {  // (BNRELU view, no dropout: checked by the caller)
+#define UNET_DWF(Q)                                                                                         \
+    dw_tile_bwd_data<UNET_VIEW_BNRELU, false, Q, true, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w,   \
+                                                                                    p.tiles_h, K, dY, dx0,   \
+                                                                                    nullptr, mu, rs, bnpart, \
+                                                                                    dwpart)
+        switch (p.qt) {
+            case 16: UNET_DWF(16); break;
+            case 8: UNET_DWF(8); break;
+            case 4: UNET_DWF(4); break;
+            case 2: UNET_DWF(2); break;
+            default: UNET_DWF(1); break;
+        }
+#undef UNET_DWF
+        UNET_CHECK_LAUNCH("dwconv3x3_bwd_data_bnstats(tiled, filter gradient)");
+        return 0;
+    }
 #define UNET_BNS(D, Q)                                                                                            \
     if (mode == UNET_VIEW_POOL_BNRELU)                                                                            \
         dw_tile_bwd_data<UNET_VIEW_POOL_BNRELU, D, Q, true><<<grid, 256, 0, st>>>(v, N, H, W, p.tiles_w, p.tiles_h, \

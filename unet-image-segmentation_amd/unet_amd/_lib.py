@@ -54,6 +54,8 @@ SIGNATURES = {
     "unet_dwconv3x3_bwd_data": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P]),
     "unet_dwconv3x3_bwd_data_bnstats_slabs": (c_int, [_VP, c_int, c_int, c_int]),
     "unet_dwconv3x3_bwd_data_bnstats": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P]),
+    "unet_dwconv3x3_bwd_data_bnstats_dwf": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, P]),
+    "unet_reduce_slabs": (c_int, [P, c_int, c_int64, P, P]),
     "unet_dwconv3x3_bwd_filter_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
     "unet_dwconv3x3_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_size_t, P]),
     "unet_bn_partials_size": (c_size_t, [c_int64, c_int]),

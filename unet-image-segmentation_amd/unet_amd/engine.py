@@ -104,6 +104,7 @@ class BlockBufs:
     y_recompute: bool = False  # last training forward kept no y: the weight grads recompute it
     zsel: Optional[torch.Tensor] = None  # encoder block2: the 2x2 max-pool selection of z (n, h/2, w/2, C)
     dlogit: Optional[torch.Tensor] = None  # last block, binary head: dL/dlogit per pixel (its da is rank one)
+    dwpart: Optional[torch.Tensor] = None  # depthwise filter-gradient slabs of the fused data + filter pass
     da_rank1: bool = False  # this backward's da is dlogit (x) the head kernel, never materialised
     rec: Optional[torch.Tensor] = None  # SyncBN: this replica's (count, mean, M2) record, float64 1 + 2C
     recs: Optional[torch.Tensor] = None  # SyncBN: the gathered records [world][1 + 2C]
@@ -209,6 +210,10 @@ class UNetEngine:
         # weight gradients from it; dz never stored) instead of the data-gradient GEMM + the
         # side-stream weight-gradient pass
         self.fuse_block_bwd = True
+        # a BN+ReLU-view block's depthwise FILTER gradient accumulated by its depthwise data-gradient pass
+        # (the same dy window, x from the z the BN statistics read): no second pass over dy and the view
+        # on the side stream; the per-tile slabs are summed there instead (round 6)
+        self.dw_fused_filter = True
         # SyncBN (SURVEY 8(e) option, off by default like tf.distribute / Keras synchronized=False):
         # under data parallelism every BatchNorm uses the global batch's statistics -- the forward
         # gathers each replica's (count, mean, M2) and combines them in rank order, the backward
@@ -720,6 +725,11 @@ class UNetEngine:
                             drop_seed, dgamma, dbeta, dz)
             ops.pointwise_bwd_data(dz, m, b.cin, b.cout, pk, dy)
         gdk, gpk = self._gwts(b)
+        # the depthwise filter gradient from the data-gradient pass (unet_dwconv3x3_bwd_data_bnstats_dwf)
+        dwf = (self.dw_fused_filter and dx0 is not None and stats_target is not None and self.fuse_bn_stats
+               and self.fuse_bn_bwd and view_in.mode == L.VIEW_BNRELU and view_in.drop_rate == 0.0
+               and view_f is view_in and not fused_bwd and not img_all and not bb.y_recompute and not b.wcin
+               and ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w) > 0)
 
         def weight_grads():
             if fused_bwd or img_all:  # (done by the fused pass)
@@ -729,7 +739,8 @@ class UNetEngine:
                 return
             if not img_wg:  # (the image block's was accumulated by its data-gradient pass)
                 ops.pointwise_bwd_filter(bb.y, dz, m, b.cin, b.cout, gpk)
-            ops.dwconv3x3_bwd_filter(view_f, n, h, w, dy, gdk)
+            if not dwf:
+                ops.dwconv3x3_bwd_filter(view_f, n, h, w, dy, gdk)
             if b.wcin:  # padded image block: keep the Keras-shaped slices
                 ops.copy_strided(gpk, 1, b.wcin * b.cout, b.cin * b.cout,
                                  self.gvars[f"{b.name}_sepconv/pointwise_kernel"], b.wcin * b.cout)
@@ -753,7 +764,16 @@ class UNetEngine:
             S = 0
             if stats_target is not None and self.fuse_bn_stats and self.fuse_bn_bwd:
                 S = ops.dwconv3x3_bwd_data_bnstats_slabs(view_in, n, h, w)
-            if S > 0:
+            if S > 0 and dwf:
+                tb, C = stats_target, view_in.channels
+                if bb.dwpart is None or bb.dwpart.numel() < S * 9 * C:
+                    bb.dwpart = torch.empty(S * 9 * C, dtype=torch.float32, device=self.device)
+                ops.dwconv3x3_bwd_data_bnstats_dwf(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
+                                                   tb.rstd if self.use_bn else None, self._bnpart(tb, S, C),
+                                                   bb.dwpart[:S * 9 * C])
+                tb.bn_slabs = S
+                self.run_beside(lambda: ops.reduce_slabs(bb.dwpart[:S * 9 * C], S, 9 * C, gdk))
+            elif S > 0:
                 tb = stats_target
                 ops.dwconv3x3_bwd_data_bnstats(view_in, n, h, w, dk, dy, dx0, tb.mean if self.use_bn else None,
                                                tb.rstd if self.use_bn else None, self._bnpart(tb, S, view_in.channels))

@@ -290,6 +290,31 @@ def dwconv3x3_bwd_data_bnstats(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Te
           _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _stream())
 
 
+def dwconv3x3_bwd_data_bnstats_dwf(x: View, n, h, w, dk: Tensor, dy: Tensor, dx0: Tensor, mean, rstd,
+                                   partials: Tensor, dw_partials: Tensor):
+    """BNRELU view (no dropout): dwconv3x3_bwd_data_bnstats that also writes the depthwise filter
+    gradient's per-tile slabs ([S][9][C]; sum them with reduce_slabs)."""
+    C = x.channels
+    S = dwconv3x3_bwd_data_bnstats_slabs(x, n, h, w)
+    _check(dk, "depthwise_kernel", 9 * C)
+    _check(dy, "dy", n * h * w * C)
+    _check(dx0, "dx0")
+    _check(partials, "bn_partials", bn_stats_partials_numel(S, C))
+    _check(dw_partials, "dw_partials", S * 9 * C)
+    vs = x.c_struct()
+    m = n * h * w
+    nb = 12.0 * m * C + 4.0 * S * 2 * C + 4.0 * S * 9 * C
+    _call("unet_dwconv3x3_bwd_data_bnstats_dwf", (36.0 * m * C, nb), ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(dy),
+          _ptr(dx0), _ptr(mean), _ptr(rstd), _ptr(partials), _ptr(dw_partials), _stream())
+
+
+def reduce_slabs(slabs: Tensor, S: int, length: int, out: Tensor):
+    """out = sum of S slabs of `length` floats, fixed order (slabs is scratch: overwritten)."""
+    _check(slabs, "slabs", S * length)
+    _check(out, "out", length)
+    _call("unet_reduce_slabs", (0.0, 4.0 * S * length), _ptr(slabs), S, length, _ptr(out), _stream())
+
+
 def dwconv3x3_bwd_filter(x: View, n, h, w, dy: Tensor, ddk: Tensor):
     C = x.channels
     _check(dy, "dy", n * h * w * C)
