@@ -1,35 +1,38 @@
 #!/bin/bash
-# usage: tools/sessions/r6_fin.sh TAG -- round-6 evidence at HEAD: GPU tests, smoke, the full bench line
+# usage: tools/sessions/r6_fin.sh TAG [A|B] -- (A: up to the step PMC passes; B: the PMC groups and other configs)
+# round-6 evidence at HEAD: GPU tests, smoke, the full bench line
 # (encoder table + CPU baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE /
 # WRITE_SIZE passes of the bench (roofline traffic, whole-step bytes), SQ / byte PMC groups on enc2_block1,
 # enc3_block1 and enc3_block2 at batch 32, and the other BASELINE configs at their per-GPU shape
 source "$(dirname "$0")/gpu_session.sh"
 TAG=${1:-r6fin}
+PART=${2:-AB}
 export UNET_PARITY_LOG=gpurun_out/parity_${TAG}.jsonl
-run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run bench 900 python bench.py
-run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o ${TAG} -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --encoder-batch 0
+[[ $PART == *A* ]] && run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+[[ $PART == *A* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[[ $PART == *A* ]] && run bench 900 python bench.py
+[[ $PART == *A* ]] && run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o ${TAG} -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --encoder-batch 0
 B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline --encoder-batch 0"
 export UNET_OVERLAP=0
-run prof1s 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o ${TAG}_1s -- $B
+[[ $PART == *A* ]] && run prof1s 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o ${TAG}_1s -- $B
 unset UNET_OVERLAP
-run pmcF 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_fetch -- $B
-run pmcW 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_write -- $B
+[[ $PART == *A* ]] && run pmcF 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_fetch -- $B
+[[ $PART == *A* ]] && run pmcW 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_write -- $B
 export N=32
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS"
 S="python tools/sep_one.py 1 128 128 64 128 10 x3"
-run e2b1F 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_fetch -- $S
-run e2b1W 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_write -- $S
-run e2b1S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_sq -- $S
+[[ $PART == *B* ]] && run e2b1F 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_fetch -- $S
+[[ $PART == *B* ]] && run e2b1W 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_write -- $S
+[[ $PART == *B* ]] && run e2b1S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e2b1_sq -- $S
 S="python tools/sep_one.py 1 64 64 128 256 10 x3"
-run e3b1S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e3b1_sq -- $S
+[[ $PART == *B* ]] && run e3b1S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e3b1_sq -- $S
 export POOL=1
 S="python tools/sep_one.py 1 64 64 256 256 10 x3"
-run e3b2S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e3b2_sq -- $S
+[[ $PART == *B* ]] && run e3b2S 120 rocprofv3 --pmc $SQ --output-format csv -d gpurun_out/pmc -o ${TAG}_e3b2_sq -- $S
 unset POOL N
-run cfg3 300 python bench.py --size 512 --batch 8 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
-run cfg4_b8 300 python bench.py --num-classes 21 --batch 8 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
-run cfg4_b32 300 python bench.py --num-classes 21 --batch 32 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
-run cfg0 300 python bench.py --size 128 --batch 2 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
-run syncbn2 300 env UNET_DP_ONE_DEVICE=1 python bench.py --gpus 2 --sync-bn --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *B* ]] && run cfg3 300 python bench.py --size 512 --batch 8 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *B* ]] && run cfg4_b8 300 python bench.py --num-classes 21 --batch 8 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *B* ]] && run cfg4_b32 300 python bench.py --num-classes 21 --batch 32 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *B* ]] && run cfg0 300 python bench.py --size 128 --batch 2 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *B* ]] && run syncbn2 300 env UNET_DP_ONE_DEVICE=1 python bench.py --gpus 2 --sync-bn --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --encoder-batch 0
+exit 0
