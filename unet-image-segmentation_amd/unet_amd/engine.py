@@ -39,9 +39,9 @@ FUSE_MIN_PIXELS = 64 * 64  # fused conv forward from the 64 x 64 level up (tools
 # batch 16 (configs[1]; with the weight planes staged by LDS-DMA its bf16x6 launch 54.8 -> 47.3 us, and
 # the step 10.44-10.47 -> 10.37-10.41 ms, profiles/r6h_fuse32_b16_ab.txt); at batch 8 (configs[4] per
 # GPU) the split launches stay faster (6.05-6.07 vs 6.15-6.16 ms)
-# (fixed at import: every data-parallel rank takes the same route; an A/B sets engine.fuse_min_total
-# or UNET_FUSE_MIN_TOTAL, which every rank inherits from the launcher)
-FUSE_MIN_TOTAL_PIXELS = int(os.environ.get("UNET_FUSE_MIN_TOTAL", 16 * 1024))
+# (a fixed constant: every data-parallel rank takes the same route; an A/B sets the engine attributes
+# fuse_min_pixels / fuse_min_total, bench.py --fuse-min-pixels / --fuse-min-total)
+FUSE_MIN_TOTAL_PIXELS = 16 * 1024
 # blocks whose weight gradients recompute y instead of the forward storing it: an output channel count
 # (64: the fused block backward), or an (input, output) channel pair
 RECOMPUTE_Y_COUTS = (64,)
