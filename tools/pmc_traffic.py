@@ -38,6 +38,8 @@ OPS = {
     "unet_sepconv_fwd": r"sepconv_(fwd|rk|px)_kernel<",
     "unet_sepconv_bwd_filter": r"sepconv_wgrad_kernel<",
     "unet_pointwise_bwd_data_bnrelu": r"gemm_rows_vec<\d+, \d+, \d+, 3, (true|false), 0, (true|false)(, (true|false))?>",
+    # (round 6: the split-precision route's launches -- X6 = true -- and the fp32 fall-backs of the same op)
+    "unet_pointwise_bwd_data_bnrelu_x3": r"gemm_rows_vec<\d+, \d+, \d+, 3, (true|false), 0, (true|false)(, (true|false))?>",
     "unet_conv_transpose2x2_bwd_data_bnstats": r"gemm_rows_vec<\d+, \d+, \d+, 2, false, 3, (true|false)(, (true|false))?>",
     "unet_pointwise_bwd_data_bnrelu_wgrad": r"img_pw_bwd_kernel<",
 }

@@ -39,7 +39,7 @@ def main():
         open(os.path.join(P, f"{tag}_step_trace.txt"), "w").write(out)
     fe, wr = one(f"pmc/**/{tag}_fetch_counter_collection.csv"), one(f"pmc/**/{tag}_write_counter_collection.csv")
     if fe and wr:  # the bench line's roofline op (the largest share of the single-stream breakdown), and the GEMM
-        ops_ = [json.loads(lines[0])["roofline"]["kernel"], "unet_pointwise_bwd_data_bnrelu"]
+        ops_ = [json.loads(lines[0])["roofline"]["kernel"], "unet_pointwise_bwd_data_bnrelu_x3"]
         for op in dict.fromkeys(ops_):
             r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), fe, wr,
                                 os.path.join(P, f"{tag}_traffic_{op[5:]}.json"), op], capture_output=True, text=True)
