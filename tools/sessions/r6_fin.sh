@@ -1,5 +1,7 @@
 #!/bin/bash
-# usage: tools/sessions/r6_fin.sh TAG [A|B] -- (A: up to the step PMC passes; B: the PMC groups and other configs)
+# usage: tools/sessions/r6_fin.sh TAG [A|B|C] -- (A: up to the step PMC passes; B: the PMC groups and other configs;
+# C: the default bench line again once the PMC traffic summary of this library build is committed, so its
+# roofline object carries the measured traffic -> profiles/r6fin_bench_pinned.log)
 # round-6 evidence at HEAD: GPU tests, smoke, the full bench line
 # (encoder table + CPU baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE /
 # WRITE_SIZE passes of the bench (roofline traffic, whole-step bytes), SQ / byte PMC groups on enc2_block1,
@@ -35,4 +37,5 @@ unset POOL N
 [[ $PART == *B* ]] && run cfg4_b32 300 python bench.py --num-classes 21 --batch 32 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
 [[ $PART == *B* ]] && run cfg0 300 python bench.py --size 128 --batch 2 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
 [[ $PART == *B* ]] && run syncbn2 300 env UNET_DP_ONE_DEVICE=1 python bench.py --gpus 2 --sync-bn --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --encoder-batch 0
+[[ $PART == *C* ]] && run bench_pinned 900 python bench.py
 exit 0
