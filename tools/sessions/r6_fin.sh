@@ -1,7 +1,9 @@
 #!/bin/bash
 # usage: tools/sessions/r6_fin.sh TAG [A|B|C] -- (A: up to the step PMC passes; B: the PMC groups and other configs;
 # C: the default bench line again once the PMC traffic summary of this library build is committed, so its
-# roofline object carries the measured traffic -> profiles/r6fin_bench_pinned.log)
+# roofline object carries the measured traffic -> profiles/r6fin_bench_pinned.log;
+# S: the fused 64-output block backward on the split-precision route -- its GPU tests, the training-
+# geometry parity, then three alternated bench pairs against --no-x6-fused-bwd -> profiles/r6sx_*)
 # round-6 evidence at HEAD: GPU tests, smoke, the full bench line
 # (encoder table + CPU baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE /
 # WRITE_SIZE passes of the bench (roofline traffic, whole-step bytes), SQ / byte PMC groups on enc2_block1,
@@ -38,4 +40,12 @@ unset POOL N
 [[ $PART == *B* ]] && run cfg0 300 python bench.py --size 128 --batch 2 --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --encoder-batch 0
 [[ $PART == *B* ]] && run syncbn2 300 env UNET_DP_ONE_DEVICE=1 python bench.py --gpus 2 --sync-bn --steps 10 --warmup 3 --no-cpu-baseline --no-roofline --encoder-batch 0
 [[ $PART == *C* ]] && run bench_pinned 900 python bench.py
+if [[ $PART == *S* ]]; then
+  run sx_tests 600 python -u -m pytest tests/test_ops_gpu.py -k sepconv_bwd_fused -x -q --timeout 300 --timeout-method thread
+  for i in 1 2 3; do
+    run ab_sx1_$i 300 python bench.py --no-cpu-baseline --no-roofline --encoder-batch 0
+    run ab_sx0_$i 300 python bench.py --no-cpu-baseline --no-roofline --encoder-batch 0 --no-x6-fused-bwd
+  done
+  run sx_prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o r6sx -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --encoder-batch 0
+fi
 exit 0
