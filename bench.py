@@ -332,8 +332,6 @@ def parse_args(argv=None):
     ap.add_argument("--no-x6-gemm", action="store_true",
                     help="fp32-MFMA rows GEMMs (BN-backward data gradient, ConvT forward / data gradient, split-"
                          "route pointwise forward) instead of their split-precision (bf16x6) route (A/B)")
-    ap.add_argument("--no-x6-fused-bwd", action="store_true",
-                    help="A/B: the fused 64-output block backward on fp32 MFMA instead of the bf16x6 route")
     ap.add_argument("--no-dw-fused-filter", action="store_true",
                     help="BN+ReLU-view blocks: depthwise filter gradient as its own side-stream pass instead of "
                          "inside the depthwise data-gradient pass (A/B)")
@@ -390,7 +388,6 @@ def main():
     model.engine.use_x3 = not args.no_x3
     model.engine.x6_gemm = not args.no_x6_gemm
     model.engine.dw_fused_filter = not args.no_dw_fused_filter
-    model.engine.x6_fused_bwd = not args.no_x6_fused_bwd
     model.engine.fuse_block_bwd = not args.no_fused_bwd
     model.engine.fuse_sepconv = args.fuse
     if args.fuse_min_pixels:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define UNET_ABI_VERSION 13
+#define UNET_ABI_VERSION 12
 
 typedef void* unet_stream_t; /* hipStream_t */
 
@@ -264,15 +264,6 @@ int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float*
                            const float* scale, const float* shift, const float* coef, int cout,
                            float* dy, float* d_dw_kernel, float* d_pw_kernel, void* ws,
                            size_t ws_bytes, unet_stream_t stream);
-/* The same on the split-precision route (ABI 13): both products (dy = dz . pw_kernel^T and
- * y^T dz) run the six significant bf16 part products of operands split exactly into bf16
- * hi + mid + lo as they are read (fp32-accurate; see unet_pointwise_bwd_data_bnrelu_x3).     */
-int unet_sepconv_bwd_fused_x3(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                              const float* pw_kernel, const float* da, const float* da_dlogit,
-                              const float* da_kernel, const float* z,
-                              const float* scale, const float* shift, const float* coef, int cout,
-                              float* dy, float* d_dw_kernel, float* d_pw_kernel, void* ws,
-                              size_t ws_bytes, unet_stream_t stream);
 
 /* ----- BatchNormalization() — model/u_net.py:22-23 (Keras defaults:
  * momentum 0.99, epsilon 1e-3, biased batch variance for both the output

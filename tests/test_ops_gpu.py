@@ -1086,13 +1086,10 @@ def test_sepconv_persistent_matches_one_tile(ops, mode, n, h, w, c0, c1, cout, d
 @pytest.mark.parametrize("mode,n,h,w,c0,c1", [(1, 2, 8, 16, 64, 0), (1, 1, 16, 32, 64, 0), (3, 1, 8, 32, 64, 64),
                                               (0, 2, 16, 16, 128, 0)])
 @pytest.mark.parametrize("use_bn", [True, False])
-@pytest.mark.parametrize("x6", [False, True])
-def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn, x6):
-    """The fused 64-output block backward (unet_sepconv_bwd_fused, and with x6 its split-precision
-    route unet_sepconv_bwd_fused_x3, ABI 13) against the route it replaces:
+def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn):
+    """The fused 64-output block backward (unet_sepconv_bwd_fused) against the route it replaces:
     unet_pointwise_bwd_data_bnrelu (dz formed on load, dy) + unet_sepconv_bwd_filter over that dz /
-    dy, and against the float64 oracle's BN + ReLU backward and weight gradients (x6: at most 1.5x
-    the fp32-MFMA route's own distance to float64, or 1e-6)."""
+    dy, and against the float64 oracle's BN + ReLU backward and weight gradients."""
     rng = np.random.default_rng(700 + mode + n + (7 if use_bn else 0))
     a, t = _view_inputs(rng, mode, n, h, w, c0, c1)
     C, cout, m = c0 + c1, 64, n * h * w
@@ -1117,7 +1114,7 @@ def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn, x6):
     v = _mk_view(ops, mode, t)
     dy_f = torch.full((n, h, w, C), 7.0, device="cuda")
     ddk_f, dpk_f = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
-    ops.sepconv_bwd_fused(v, n, h, w, dk, pk, tda, tz, ts, th, coef, cout, dy_f, ddk_f, dpk_f, x6=x6)
+    ops.sepconv_bwd_fused(v, n, h, w, dk, pk, tda, tz, ts, th, coef, cout, dy_f, ddk_f, dpk_f)
     dy_r, dz_r = torch.empty((m, C), device="cuda"), torch.empty((m, cout), device="cuda")
     ops.pointwise_bwd_data_bnrelu(tda, tz, m, C, cout, pk, ts, th, coef, 0.0, 0, dy_r, dz_r)
     ddk_r, dpk_r = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
@@ -1134,10 +1131,9 @@ def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn, x6):
         dy1 = torch.full((n, h, w, C), 7.0, device="cuda")
         ddk1, dpk1 = torch.empty((3, 3, C, 1), device="cuda"), torch.empty((1, 1, C, cout), device="cuda")
         if r1:
-            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, None, tz, ts, th, coef, cout, dy1, ddk1, dpk1, da_rank1=(dlg, hk),
-                                  x6=x6)
+            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, None, tz, ts, th, coef, cout, dy1, ddk1, dpk1, da_rank1=(dlg, hk))
         else:
-            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, da1, tz, ts, th, coef, cout, dy1, ddk1, dpk1, x6=x6)
+            ops.sepconv_bwd_fused(v, n, h, w, dk, pk, da1, tz, ts, th, coef, cout, dy1, ddk1, dpk1)
         outs1.append((dy1, ddk1, dpk1))
     for x1, x2 in zip(*outs1):
         assert torch.equal(x1, x2)
@@ -1152,12 +1148,4 @@ def test_sepconv_bwd_fused(ops, mode, n, h, w, c0, c1, use_bn, x6):
     xv = view_value(mode, a["src0"], a.get("sc0"), a.get("sh0"), a.get("src1"), a.get("sc1"), a.get("sh1"),
                     0.0, 0).astype(np.float64)
     yr = K.depthwise3x3(xv, host(dk).astype(np.float64))
-    rpk = yr.reshape(m, C).T @ rz
-    assert rel_err(host(dpk_f).reshape(C, cout), rpk) < 1e-4
-    if x6:  # the split route is as close to float64 as the fp32-MFMA route
-        dy_3, ddk_3, dpk_3 = torch.empty_like(dy_f), torch.empty_like(ddk_f), torch.empty_like(dpk_f)
-        ops.sepconv_bwd_fused(v, n, h, w, dk, pk, tda, tz, ts, th, coef, cout, dy_3, ddk_3, dpk_3)
-        for got, fp32, ref in ((dy_f, dy_3, ry), (dpk_f, dpk_3, rpk)):
-            e6 = rel_err(host(got).reshape(ref.shape), ref)
-            e32 = rel_err(host(fp32).reshape(ref.shape), ref)
-            assert e6 <= max(1.5 * e32, 1e-6), (e6, e32)
+    assert rel_err(host(dpk_f).reshape(C, cout), yr.reshape(m, C).T @ rz) < 1e-4

@@ -2,7 +2,7 @@
 # usage: tools/sessions/r6_fin.sh TAG [A|B|C] -- (A: up to the step PMC passes; B: the PMC groups and other configs;
 # C: the default bench line again once the PMC traffic summary of this library build is committed, so its
 # roofline object carries the measured traffic -> profiles/r6fin_bench_pinned.log;
-# S: the fused 64-output block backward on the split-precision route -- its GPU tests, the training-
+# S (commit 035656c, reverted after it: the route and its flag are gone): the fused 64-output block backward on the split-precision route -- its GPU tests, the training-
 # geometry parity, then three alternated bench pairs against --no-x6-fused-bwd -> profiles/r6sx_*)
 # round-6 evidence at HEAD: GPU tests, smoke, the full bench line
 # (encoder table + CPU baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE /

@@ -84,14 +84,6 @@ __device__ __forceinline__ Split4 split4(float4 v) {
     s.l = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
     return s;
 }
-// 8 consecutive k of one MFMA operand row / column -> its hi, mid, lo bf16x8 fragments
-__device__ __forceinline__ void split8(const float* x, bf16x8* o) {
-    const Split4 s0 = split4(make_float4(x[0], x[1], x[2], x[3]));
-    const Split4 s1 = split4(make_float4(x[4], x[5], x[6], x[7]));
-    o[0] = __builtin_bit_cast(bf16x8, make_uint4(s0.h.x, s0.h.y, s1.h.x, s1.h.y));
-    o[1] = __builtin_bit_cast(bf16x8, make_uint4(s0.m.x, s0.m.y, s1.m.x, s1.m.y));
-    o[2] = __builtin_bit_cast(bf16x8, make_uint4(s0.l.x, s0.l.y, s1.l.x, s1.l.y));
-}
 // acc += a.b over the six significant products of the split operands (a[0..2] = hi, mid, lo)
 __device__ __forceinline__ floatx16 mfma_x6(const bf16x8* a, const bf16x8* b, floatx16 acc) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);

@@ -44,7 +44,6 @@ struct SwArgs {
     const float *da, *z, *coef, *bsc, *bsh, *pk;
     const float *da_dl, *da_k;  // rank-one da = da_dl[px] * da_k[c] (the binary head), da NULL
     float* dy_out;
-    bool x6;  // fused kernel: both products on the split-precision route (unet_sepconv_bwd_fused_x3)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -72,12 +71,7 @@ static_assert(CI * CO <= SIZE && 9 * 16 * 16 * 4 <= SIZE, "epilogue scratch");
 static_assert(2 * SIZE * 4 <= 160 * 1024, "two blocks per CU");
 }  // namespace fb
 
-// X6: both products on the bf16 MFMA with every operand split into bf16 hi / mid / lo as it is read
-// from LDS (8 consecutive k per lane and 16-deep step: dz and the Wt copy for dy, y and dz for
-// y^T dz; common.h split8 / mfma_x6): 6 x 32 instead of 8 x 64 matrix cycles per 16 deep, and the
-// FP32 datapath left to the VALU phases (dz formation, y recompute, depthwise filter gradient).
-// (A register-resident copy of pre-split pk fragments needs 48 more VGPRs and spills.)
-template <int MODE, bool DA1 = false, bool X6 = false>
+template <int MODE, bool DA1 = false>
 __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) {
     constexpr int TH = fb::TH, TW = fb::TW, HWp = fb::HWp, PX = fb::PX, NT = fb::NT, CI = fb::CI, CO = fb::CO;
     constexpr int ZS = fb::ZS, NHQ = fb::NHQ, HR = fb::HR, DQ = fb::DQ;
@@ -205,6 +199,7 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
     float4 dwa[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) dwa[t] = f4(0.f);
+
     if (t_begin < t_end) load(t_begin);
     for (int T = t_begin; T < t_end; ++T) {
         if constexpr (!(SW_KO & 8)) store();
@@ -217,26 +212,10 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
             floatx16 ad;
 #pragma unroll
             for (int r = 0; r < 16; ++r) ad[r] = 0.f;
-            if constexpr (X6) {
-#pragma unroll
-                for (int ks = 0; ks < CO / 16; ++ks) {
-                    float a8[8], b8[8];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        a8[e] = Zs[(px0 + lo) * ZS + 16 * ks + 8 * hi + e];
-                        b8[e] = Wt[(16 * ks + 8 * hi + e) * CI + cl0 + lo];
-                    }
-                    bf16x8 af[3], bfr[3];
-                    split8(a8, af);
-                    split8(b8, bfr);
-                    ad = mfma_x6(af, bfr, ad);
-                }
-            } else {
 #pragma unroll 8
-                for (int k = 0; k < ((SW_KO & 16) ? 0 : CO); k += 2)
-                    ad = __builtin_amdgcn_mfma_f32_32x32x2f32(Zs[(px0 + lo) * ZS + k + hi], Wt[(k + hi) * CI + cl0 + lo],
-                                                              ad, 0, 0, 0);
-            }
+            for (int k = 0; k < ((SW_KO & 16) ? 0 : CO); k += 2)
+                ad = __builtin_amdgcn_mfma_f32_32x32x2f32(Zs[(px0 + lo) * ZS + k + hi], Wt[(k + hi) * CI + cl0 + lo], ad,
+                                                          0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 16; ++r) YD[(px0 + acc_row(r, hi)) * CI + cl0 + lo] = ad[r];
         }
@@ -259,27 +238,10 @@ __global__ __launch_bounds__(fb::NT, 2) void sepconv_bwd_fused_kernel(SwArgs g) 
             *yd = y;  // the same thread read this slot's dy above
         }
         __syncthreads();
-        if constexpr (X6) {
-#pragma unroll
-            for (int ks = 0; ks < PX / 16; ++ks) {
-                float a8[8], b8[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int p = 16 * ks + 8 * hi + e;
-                    a8[e] = YD[p * CI + wci + lo];
-                    b8[e] = Zs[p * ZS + wco + lo];
-                }
-                bf16x8 af[3], bfr[3];
-                split8(a8, af);
-                split8(b8, bfr);
-                acc = mfma_x6(af, bfr, acc);
-            }
-        } else {
 #pragma unroll 4
-            for (int s = 0; s < ((SW_KO & 1) ? 0 : PX / 2); ++s) {
-                const int p = 2 * s + hi;
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(YD[p * CI + wci + lo], Zs[p * ZS + wco + lo], acc, 0, 0, 0);
-            }
+        for (int s = 0; s < ((SW_KO & 1) ? 0 : PX / 2); ++s) {
+            const int p = 2 * s + hi;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(YD[p * CI + wci + lo], Zs[p * ZS + wco + lo], acc, 0, 0, 0);
         }
         __syncthreads();
     }
@@ -532,9 +494,7 @@ SwPlan sw_plan(int n, int h, int w, int cin) {
 
 template <int MODE, bool DROP>
 void launch_sw(const SwArgs& a, int cout, int blocks, hipStream_t st) {
-    if (a.da_dl && a.x6) sepconv_bwd_fused_kernel<MODE, true, true><<<blocks, fb::NT, 0, st>>>(a);
-    else if (a.da_dl) sepconv_bwd_fused_kernel<MODE, true><<<blocks, fb::NT, 0, st>>>(a);
-    else if (a.da && a.x6) sepconv_bwd_fused_kernel<MODE, false, true><<<blocks, fb::NT, 0, st>>>(a);
+    if (a.da_dl) sepconv_bwd_fused_kernel<MODE, true><<<blocks, fb::NT, 0, st>>>(a);
     else if (a.da) sepconv_bwd_fused_kernel<MODE><<<blocks, fb::NT, 0, st>>>(a);
     else if (cout == 128) sepconv_bwd_filter2_kernel<MODE, DROP, 128><<<blocks, fb::NT, 0, st>>>(a);
     else sepconv_bwd_filter2_kernel<MODE, DROP, 64><<<blocks, fb::NT, 0, st>>>(a);
@@ -606,12 +566,12 @@ int run_sw(const unet_view* x, int n, int h, int w, const float* dw_kernel, SwAr
 }
 }  // namespace
 
-namespace {
-int sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel, const float* pw_kernel,
-                      bool x6, const float* da, const float* da_dlogit, const float* da_kernel,
-                      const float* z, const float* scale, const float* shift, const float* coef, int cout, float* dy,
-                      float* d_dw_kernel, float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream,
-                      const char* op) {
+extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
+                                      const float* pw_kernel, const float* da, const float* da_dlogit,
+                                      const float* da_kernel, const float* z, const float* scale,
+                                      const float* shift, const float* coef, int cout, float* dy, float* d_dw_kernel,
+                                      float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
+    const char* op = "unet_sepconv_bwd_fused";
     if (check_view(x, op)) return -1;
     UNET_CHECK_ARG(cout == 64 && unet_sepconv_bwd_filter_supported(x, n, h, w, cout) && x->drop_rate == 0.f,
                    "%s: unsupported (needs 64 output channels, input channels %% 64 == 0, no dropout on the input, "
@@ -633,29 +593,8 @@ int sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_k
     a.bsc = scale;
     a.bsh = shift;
     a.pk = pw_kernel;
-    a.x6 = x6;
     a.dy_out = dy;
     return run_sw(x, n, h, w, dw_kernel, a, cout, d_dw_kernel, d_pw_kernel, ws, ws_bytes, stream, op);
-}
-}  // namespace
-
-extern "C" int unet_sepconv_bwd_fused(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                                      const float* pw_kernel, const float* da, const float* da_dlogit,
-                                      const float* da_kernel, const float* z, const float* scale,
-                                      const float* shift, const float* coef, int cout, float* dy, float* d_dw_kernel,
-                                      float* d_pw_kernel, void* ws, size_t ws_bytes, unet_stream_t stream) {
-    return sepconv_bwd_fused(x, n, h, w, dw_kernel, pw_kernel, false, da, da_dlogit, da_kernel, z, scale, shift,
-                             coef, cout, dy, d_dw_kernel, d_pw_kernel, ws, ws_bytes, stream, "unet_sepconv_bwd_fused");
-}
-
-extern "C" int unet_sepconv_bwd_fused_x3(const unet_view* x, int n, int h, int w, const float* dw_kernel,
-                                         const float* pw_kernel, const float* da, const float* da_dlogit,
-                                         const float* da_kernel, const float* z, const float* scale,
-                                         const float* shift, const float* coef, int cout, float* dy,
-                                         float* d_dw_kernel, float* d_pw_kernel, void* ws, size_t ws_bytes,
-                                         unet_stream_t stream) {
-    return sepconv_bwd_fused(x, n, h, w, dw_kernel, pw_kernel, true, da, da_dlogit, da_kernel, z, scale, shift,
-                             coef, cout, dy, d_dw_kernel, d_pw_kernel, ws, ws_bytes, stream, "unet_sepconv_bwd_fused_x3");
 }
 
 extern "C" int unet_sepconv_bwd_filter(const unet_view* x, int n, int h, int w, const float* dw_kernel,

@@ -12,7 +12,7 @@ from pathlib import Path
 
 LIB_NAME = "libunet_hip.so"
 LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
-ABI_VERSION = 13
+ABI_VERSION = 12
 SPLIT_MAX_SEGS = 64  # UNET_SPLIT_MAX_SEGS
 
 VIEW_PLAIN, VIEW_BNRELU, VIEW_POOL_BNRELU, VIEW_CONCAT = 0, 1, 2, 3
@@ -75,8 +75,6 @@ SIGNATURES = {
     "unet_sepconv_bwd_filter": (c_int, [_VP, c_int, c_int, c_int, P, P, P, c_int, P, P, P, c_size_t, P]),
     "unet_sepconv_bwd_fused": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, P,
                                        c_size_t, P]),
-    "unet_sepconv_bwd_fused_x3": (c_int, [_VP, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P,
-                                          P, c_size_t, P]),
     "unet_sepconv_set_schedule": (c_int, [c_int]),
     "unet_bn_finalize": (c_int, [P, c_int64, c_int, P, P, c_float, c_float, P, P, c_int, P, P, P, P, P]),
     "unet_bn_moments": (c_int, [P, c_int64, c_int, P, P]),

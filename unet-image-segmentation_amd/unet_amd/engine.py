@@ -210,9 +210,6 @@ class UNetEngine:
         # weight gradients from it; dz never stored) instead of the data-gradient GEMM + the
         # side-stream weight-gradient pass
         self.fuse_block_bwd = True
-        # ... with both of its products on the split-precision (bf16x6) route (unet_sepconv_bwd_fused_x3,
-        # round 6)
-        self.x6_fused_bwd = True
         # a BN+ReLU-view block's depthwise FILTER gradient accumulated by its depthwise data-gradient pass
         # (the same dy window, x from the z the BN statistics read): no second pass over dy and the view
         # on the side stream; the per-tile slabs are summed there instead (round 6)
@@ -713,12 +710,11 @@ class UNetEngine:
                 gdk_f, gpk_f = self._gwts(b)
                 if bb.da_rank1:  # the binary head's da = dlogit (x) kernel, formed on load
                     ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, None, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
-                                          dy, gdk_f, gpk_f, da_rank1=(bb.dlogit, self.vars["output_mask/kernel"]),
-                                          x6=self.x6_fused_bwd)
+                                          dy, gdk_f, gpk_f, da_rank1=(bb.dlogit, self.vars["output_mask/kernel"]))
                     bb.da_rank1 = False
                 else:
                     ops.sepconv_bwd_fused(view_f, n, h, w, dk, pk, bb.da, bb.z, bb.scale, bb.shift, bb.coef, b.cout,
-                                          dy, gdk_f, gpk_f, x6=self.x6_fused_bwd)
+                                          dy, gdk_f, gpk_f)
             else:
                 ops.pointwise_bwd_data_bnrelu(bb.da, bb.z, m, b.cin, b.cout, pk, bb.scale, bb.shift, bb.coef,
                                               drop_rate, drop_seed, dy, dz, pkd=self._pkd(b))

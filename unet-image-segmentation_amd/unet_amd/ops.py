@@ -445,12 +445,11 @@ def sepconv_bwd_filter_supported(x: View, n: int, h: int, w: int, cout: int) -> 
 
 def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, da: Optional[Tensor], z: Tensor,
                       scale: Tensor, shift: Tensor, coef: Tensor, cout: int, dy: Tensor, ddk: Tensor, dpk: Tensor,
-                      da_rank1: Optional[Tuple[Tensor, Tensor]] = None, x6: bool = False):
+                      da_rank1: Optional[Tuple[Tensor, Tensor]] = None):
     """A 64-output block's BN + ReLU backward, pointwise data gradient and both weight gradients
     in one pass (dz never stored): dy out, d_depthwise / d_pointwise kernels overwritten.
     da_rank1 = (dlogit (m,), head kernel (cout,)) instead of da: the binary head's rank-one
-    gradient, formed on load.  x6: both products on the split-precision (bf16x6) route
-    (unet_sepconv_bwd_fused_x3)."""
+    gradient, formed on load."""
     C = x.channels
     m = n * h * w
     _check(dk, "depthwise_kernel", 9 * C)
@@ -471,11 +470,11 @@ def sepconv_bwd_fused(x: View, n: int, h: int, w: int, dk: Tensor, pk: Tensor, d
     _check(dpk, "d_pointwise_kernel", C * cout)
     ws, wsb = _ws(L.query("unet_sepconv_bwd_filter_workspace", n, h, w, C, cout), dy.device)
     vs = x.c_struct()
-    work = (4.0 * m * C * cout + 36.0 * m * C, x.src_bytes(n, h, w) + 4.0 * (m * C + m * cout) + da_bytes)
-    rest = (_ptr(da), _ptr(da_rank1[0] if da_rank1 else None), _ptr(da_rank1[1] if da_rank1 else None), _ptr(z),
-            _ptr(scale), _ptr(shift), _ptr(coef), cout, _ptr(dy), _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
-    _call("unet_sepconv_bwd_fused_x3" if x6 else "unet_sepconv_bwd_fused", work, ctypes.byref(vs), n, h, w,
-          _ptr(dk), _ptr(pk), *rest)
+    _call("unet_sepconv_bwd_fused", (4.0 * m * C * cout + 36.0 * m * C,
+                                     x.src_bytes(n, h, w) + 4.0 * (m * C + m * cout) + da_bytes),
+          ctypes.byref(vs), n, h, w, _ptr(dk), _ptr(pk), _ptr(da), _ptr(da_rank1[0] if da_rank1 else None),
+          _ptr(da_rank1[1] if da_rank1 else None), _ptr(z), _ptr(scale), _ptr(shift), _ptr(coef), cout,
+          _ptr(dy), _ptr(ddk), _ptr(dpk), ws, wsb, _stream())
 
 
 def sepconv_bwd_filter(x: View, n: int, h: int, w: int, dk: Tensor, dy: Tensor, dz: Tensor, cout: int,
