@@ -3,7 +3,8 @@
 # C: the default bench line again once the PMC traffic summary of this library build is committed, so its
 # roofline object carries the measured traffic -> profiles/r6fin_bench_pinned.log;
 # S (commit 035656c, reverted after it: the route and its flag are gone): the fused 64-output block backward on the split-precision route -- its GPU tests, the training-
-# geometry parity, then three alternated bench pairs against --no-x6-fused-bwd -> profiles/r6sx_*)
+# geometry parity, then three alternated bench pairs against --no-x6-fused-bwd -> profiles/r6sx_*;
+# G: inference through the captured HIP graph -- its GPU test, then eager vs graph latency -> profiles/r6g_*)
 # round-6 evidence at HEAD: GPU tests, smoke, the full bench line
 # (encoder table + CPU baseline), rocprofv3 kernel-trace stats (two-stream and single-stream), FETCH_SIZE /
 # WRITE_SIZE passes of the bench (roofline traffic, whole-step bytes), SQ / byte PMC groups on enc2_block1,
@@ -47,5 +48,9 @@ if [[ $PART == *S* ]]; then
     run ab_sx0_$i 300 python bench.py --no-cpu-baseline --no-roofline --encoder-batch 0 --no-x6-fused-bwd
   done
   run sx_prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o r6sx -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --encoder-batch 0
+fi
+if [[ $PART == *G* ]]; then
+  run g_tests 600 python -u -m pytest tests/test_graph_predict_gpu.py -x -v --timeout 300 --timeout-method thread
+  run g_predict 300 python tools/bench_predict.py 1 2 4 16 32
 fi
 exit 0

@@ -222,6 +222,11 @@ class UNetEngine:
         self.sync_group = None
         self.sync_world = 1
         self.sync_global_n = 0  # images in the global batch of the current step (model.train_step)
+        # inference forward captured as a HIP graph per input shape (hipGraph through torch.cuda.CUDAGraph):
+        # one graph launch replays the forward's ~60 kernel launches, so small-batch inference is not
+        # bound by the host's per-launch cost.  Opt-in (UNET_GRAPH_PREDICT=1 or this attribute).
+        self.graph_predict = os.environ.get("UNET_GRAPH_PREDICT", "0") == "1"
+        self._pgraphs: Dict[tuple, tuple] = {}
         self._pending_side = None
         self._pending_ready: Optional[str] = None
         self._ev = None  # created on first use (on the device)
@@ -410,6 +415,7 @@ class UNetEngine:
         return a
 
     def release_buffers(self):
+        self._pgraphs.clear()  # (the captured inference graphs read these buffers)
         self._acts.clear()
 
     # ------------------------------------------------------------------ forward ------
@@ -891,4 +897,35 @@ class UNetEngine:
 
     def predict(self, x: torch.Tensor) -> torch.Tensor:
         """Inference forward (BN moving stats, no dropout); returns a new (N, H, W, ncls) tensor."""
+        if self.graph_predict:
+            return self._predict_graph(x)
         return self.forward(x, training=False).clone()
+
+    def _predict_graph(self, x: torch.Tensor) -> torch.Tensor:
+        """predict() through a HIP graph: per input shape (and routing attributes) the forward is
+        run once eagerly on the graph's own stream -- every activation buffer and workspace is
+        allocated there, outside the capture -- then captured; later calls copy x into the captured
+        input and replay.  The graph reads the weights, moving statistics and split planes through
+        their device pointers, so weight updates between calls are seen (the planes are re-split
+        inside the graph, as the eager forward does)."""
+        if x.dim() != 4 or tuple(x.shape[1:]) != (self.h, self.w, self.c):
+            raise ValueError(f"expected input (N, {self.h}, {self.w}, {self.c}), got {tuple(x.shape)}")
+        key = (tuple(x.shape), self.fuse_min_pixels, self.fuse_min_total, self.use_x3, self.params.data_ptr(),
+               self.x3buf.data_ptr() if getattr(self, "x3buf", None) is not None else 0)
+        ent = self._pgraphs.get(key)
+        if ent is None:
+            st = torch.cuda.Stream(device=self.device)  # one per graph: its workspace is never regrown
+            xs = torch.empty(x.shape, dtype=torch.float32, device=self.device)
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                xs.copy_(x)
+                self.forward(xs, training=False)
+            st.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                out = self.forward(xs, training=False)
+            ent = self._pgraphs[key] = (g, xs, out, st)
+        g, xs, out, _ = ent
+        xs.copy_(x)
+        g.replay()
+        return out.clone()
